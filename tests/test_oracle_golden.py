@@ -1,0 +1,130 @@
+"""Pin the CPU oracle against fixtures produced by running the reference itself
+(tests/golden/make_golden.py).  No GPU needed."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import codec, encoder, environment, mcts, net, rules, selfplay
+
+
+def test_codec_matches_reference_json(golden):
+    g = golden('codec')
+    assert hashlib.sha256(codec.moves_dict_json().encode()).hexdigest() == g['sha256']
+    assert codec.NUM_ACTIONS == g['num_actions'] == 554
+
+
+def test_encoder_matches_reference(golden):
+    for row in golden('encoder'):
+        tok, clk = encoder.encode(row['fen'])
+        assert tok.tolist() == row['tokens'], row['fen']
+        assert float(clk) == row['clock'], row['fen']
+
+
+def test_environment_consumption_matches_reference(golden):
+    g = golden('env')
+    for row in g['positions']:
+        ep = environment.MinitChessEpisode(row['fen'])
+        assert ep.get_legal_moves() == row['legal'], row['fen']
+        assert ep.is_done() == row['done'] and ep.get_reward() == row['reward'] and ep.turn == row['turn']
+    for row in g['steps']:
+        ep = environment.MinitChessEpisode(row['fen'])
+        st = ep.step(row['code'])
+        assert (st.observation, st.reward, st.done) == (row['next'], row['reward'], row['done'])
+
+
+def test_fen_roundtrip_and_illegal_move():
+    b = rules.Board(rules.STARTING_FEN)
+    assert b.fen() == rules.STARTING_FEN
+    ep = environment.MinitChessEpisode(rules.STARTING_FEN)
+    with pytest.raises(environment.IlegalMoveException):
+        ep.step(0)          # a1b2: own bishop on b2? no - a1 king onto own pawn square b2
+    assert issubclass(environment.IlegalMoveException, BaseException)
+    assert not issubclass(environment.IlegalMoveException, Exception)
+
+
+def test_numpy_rng_streams(golden):
+    """The legacy RandomState streams the reference consumes (exp/agent.py:82,115,118)."""
+    for row in golden('rng'):
+        rs = np.random.RandomState(row['seed'])
+        for op in row['ops']:
+            if op['op'] == 'dirichlet':
+                assert rs.dirichlet([0.6] * op['k']).tolist() == op['out']
+            elif op['op'] == 'choice_p':
+                assert int(rs.choice(list(range(100, 100 + len(op['p']))), p=op['p'])) == op['out']
+            else:
+                assert int(rs.choice(np.arange(op['m']))) == op['out']
+        assert int(rs.get_state()[2]) == row['final_pos']
+
+
+def test_seed0_weights_and_outputs(golden):
+    g = golden('net')
+    n = net.seed0_network()
+    assert net.state_dict_sha256(n) == g['state_dict_sha256']
+    import torch
+    z = np.load(__import__('os').path.join(__import__('conftest').GOLDEN, 'net.npz'))
+    with torch.no_grad():
+        for i, fen in enumerate(z['fens'][:8]):
+            p, v = n(encoder.process_observation(str(fen)))
+            assert np.array_equal(p[0].numpy(), z['logits'][i])
+            assert np.float32(v.item()) == z['values'][i]
+
+
+def _check_games(games, evaluator):
+    for gm in games:
+        recs = selfplay.play_games(evaluator, 1, gm['sims'], seed_base=gm['seed'])
+        got = recs[0]
+        assert len(got) == len(gm['moves'])
+        for a, b in zip(got, gm['moves']):
+            assert a['observation'] == b['observation']
+            assert [int(x) for x in a['legal_moves']] == b['legal_moves']
+            assert a['pi'] == b['pi']
+            assert a['action'] == b['action']
+            assert a['reward'] == b['reward']
+
+
+def test_selfplay_synthetic_matches_reference(golden):
+    t = golden('trees')
+    _check_games(t['synthetic'][:3], mcts.SyntheticEvaluator(salt=t['synthetic_salt']))
+
+
+@pytest.mark.slow
+def test_selfplay_synthetic_64sims_matches_reference(golden):
+    t = golden('trees')
+    _check_games(t['synthetic'][3:], mcts.SyntheticEvaluator(salt=t['synthetic_salt']))
+
+
+@pytest.mark.slow
+def test_selfplay_seed0_net_matches_reference(golden):
+    t = golden('trees')
+    _check_games(t['net_seed0'], mcts.TorchNetEvaluator(net.seed0_network()))
+
+
+def test_terminal_revisit_quirk(golden):
+    """exp/agent.py:75-77 backs up -terminal on revisits: mating edge Q goes +1, 0, -1/3."""
+    ev = mcts.SyntheticEvaluator(salt=0)
+    for row in golden('quirk'):
+        env = environment.MinitChessEnvironment()
+        m = mcts.MonteCarloTreeSearch(env, ev, 1, rng=np.random.RandomState(0))
+        qs, ns = [], []
+        for _ in range(len(row['Q_after_each_sim'])):
+            m.simulate(1, row['fen'])
+            qs.append(m['Q'][row['fen']].tolist() if row['fen'] in m['Q'] else None)
+            ns.append(m['N'][row['fen']].tolist() if row['fen'] in m['N'] else None)
+        assert qs == row['Q_after_each_sim']
+        assert m['N'][row['fen']].tolist() == row['N_final']
+        # locate mating edges and check the quirk sequence explicitly
+        seen_quirk = False
+        for i, code in enumerate(row['legal']):
+            ep = environment.MinitChessEpisode(row['fen'])
+            st = ep.step(code)
+            if st.done and st.reward == 1.0:
+                seq, last_n = [], 0
+                for q, n in zip(qs, ns):
+                    if n is not None and n[i] != last_n:
+                        seq.append(q[i])
+                        last_n = n[i]
+                if len(seq) >= 3:
+                    assert seq[:3] == [1.0, 0.0, -1.0 / 3.0]
+                    seen_quirk = True
+        assert seen_quirk
