@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Self-play throughput benchmark (BASELINE.json metric, config 2 / config 4).
+
+A "step" = one complete self-play batch: every one of the G game slots on every
+GPU plays a full episode from STARTING_FEN at `sims` MCTS simulations per move
+(network, tree search, Dirichlet noise, action sampling all inside the timed
+region).  value = games finished by all ranks / max-over-ranks wall time.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]
+        N>1 under torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/
+        WORLD_SIZE from the env).  Games shard by global id: rank r plays seeds
+        r*G .. r*G+G-1, no collective on the data path.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = 'self-play games/sec + MCTS sims/sec at 1/2/4/8 MI355X (fixed sims/move)'
+FP32_MATRIX_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md chip table (f32-input MFMA = f32 vector rate)
+
+
+def cpu_baseline(sims, threads, seconds_cap):
+    """The oracle's restatement of the app/puppet CPU path (batch-1 torch-CPU fp32 per
+    leaf, FEN-keyed dict tables, Python rules), timed on this host: one full seeded game."""
+    import torch
+    from oracle.mcts import TorchNetEvaluator
+    from oracle.net import seed0_network
+    from oracle import selfplay
+    torch.set_num_threads(threads)
+    ev = TorchNetEvaluator(seed0_network())
+    st = {}
+    selfplay.play_games(ev, 1, sims, seed_base=0, stats=st)
+    s = st['seconds']
+    return {'value': 1.0 / s, 'unit': 'games/s', 'cores': threads, 'kind': 'port',
+            'sample': f'1 full self-play game (seed 0, {st["plies"]} plies, {sims} sims/move, {st["nn_evals"]} NN evals), '
+                      f'oracle restatement of app/puppet (batch-1 torch CPU fp32, dict tables, Python rules)',
+            'seconds': round(s, 3), 'sims_per_s': st['plies'] * sims / s, 'nn_evals_per_s': st['nn_evals'] / s}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=1)
+    ap.add_argument('--warmup', type=int, default=0)
+    ap.add_argument('--games', type=int, default=4096, help='parallel games per GPU (BASELINE config 2: 4096)')
+    ap.add_argument('--sims', type=int, default=64, help='MCTS simulations per move (config 2: 64)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-threads', type=int, default=0)
+    ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = local
+
+    from minitchess_alphazero_amd.build import build
+    if rank == 0 or world == 1:
+        build(verbose=False)
+    if dist is not None:
+        dist.barrier()
+    from minitchess_alphazero_amd.engine import Engine, FLOP_PER_CONV_BOARD, FLOP_PER_EVAL, start_position
+    from minitchess_alphazero_amd.network import Network
+
+    G, sims = args.games, args.sims
+    eng = Engine(n_games=G, sims=sims, device=device, seed_base=rank * G)
+    torch.manual_seed(0)                      # random-init weights of the reference architecture
+    eng.set_weights(Network())
+    eng.set_timing(True)
+    eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
+    for _ in range(args.warmup):
+        eng.play()
+
+    def sync():
+        torch.cuda.synchronize(device)
+        if dist is not None:
+            dist.barrier()
+
+    tot = {'sims': 0.0, 'nn_evals': 0.0, 'plies': 0.0, 'trunk_ms': 0.0, 'trunk_boards': 0.0, 'waves': 0.0,
+           'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0}
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = eng.play()
+        for k in tot:
+            tot[k] += st[k]
+    sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=torch.device('cuda', device))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        s = torch.tensor([tot[k] for k in tot], dtype=torch.float64, device=torch.device('cuda', device))
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        tot = dict(zip(tot, s.tolist()))
+    games = G * args.steps * world
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    # roofline of the dominant kernel (k_conv3x3, 18 launches per simulation wave):
+    # algorithmic FLOP per launch = boards in the launch x 2*30*256*2304, duration from
+    # HIP events around the 18 trunk launches on the engine's stream.
+    launches = 18 * tot['waves']
+    conv_ms_avg = tot['trunk_ms'] / launches if launches else float('nan')
+    flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / launches if launches else float('nan')
+    achieved = flop_per_launch / (conv_ms_avg * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get('games') == args.games and tj.get('sims') == args.sims:
+                traffic = tj.get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    line = {
+        'metric': METRIC,
+        'value': games / dt,
+        'unit': 'games/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': dt * 1e3 / args.steps,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'fp32',
+        'data': 'synthetic: self-play from STARTING_FEN, random-init weights (torch.manual_seed(0); Network())',
+        'config': {'workload': f'{G} parallel self-play games per GPU, {sims} sims/move, random-init policy net '
+                               f'(BASELINE config 2; config 4 = 8 GPUs x 4096)',
+                   'games_per_gpu': G, 'sims_per_move': sims, 'parallelism': f'games sharded over {world} GPU(s)'},
+        'sims_per_s': tot['sims'] / dt,
+        'nn_evals_per_s': tot['nn_evals'] / dt,
+        'plies_per_game': tot['plies'] / games,
+        'nn_evals_per_game': tot['nn_evals'] / games,
+        'terminal_sims_per_game': tot['terminal_sims'] / games,
+        'decisive_games': int(tot['decisive']),
+        'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12,
+        'roofline': {'bound': 'mfma', 'kernel': 'k_conv3x3 (fp32 MFMA 32x32x2)', 'achieved': achieved,
+                     'peak': FP32_MATRIX_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_MATRIX_PEAK_TFLOPS,
+                     'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch},
+        'host_rng_s': tot['host_rng_ms'] / 1e3,
+        'host_sync_s': tot['sync_ms'] / 1e3,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        line['cpu_baseline'] = cpu_baseline(sims, threads, 120)
+        line['vs_cpu_baseline'] = line['value'] / line['cpu_baseline']['value']
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,142 @@
+/* mtaz — MI355X-native AlphaZero self-play engine for MinitChess: C ABI.
+ *
+ * Drop-in boundary for the reference's self-play hot path.  The
+ * reference path is pure Python (exp/agent.py + exp/environment.py + exp/policy.py,
+ * driven by app/base.py:SimulatePuppet); every entry point below names the reference
+ * interface it replaces.  Plain pointers and sizes only; "d_" pointers are device
+ * (HBM) pointers, everything else is host memory.  Positions are 5 x uint32 packed
+ * keys (see minitchess_alphazero_amd/csrc/rules.h: struct Pos).
+ *
+ * Return convention: 0 (or a non-negative count) on success, negative on failure
+ * with mtaz_last_error() describing it.  MTAZ_E_ILLEGAL / MTAZ_E_TERMINATED map to
+ * the reference's IlegalMoveException / TerminatedEpisodeStepException
+ * (exp/environment.py:8-13), which the Python layer re-raises as BaseException
+ * subclasses exactly like the reference.
+ */
+#ifndef MTAZ_H
+#define MTAZ_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTAZ_ABI_VERSION 1
+
+#define MTAZ_E_FAIL (-1)
+#define MTAZ_E_ILLEGAL (-2)     /* exp/environment.py:11 IlegalMoveException          */
+#define MTAZ_E_TERMINATED (-3)  /* exp/environment.py:8  TerminatedEpisodeStepException */
+#define MTAZ_E_DEVICE (-4)
+#define MTAZ_E_CAPACITY (-5)
+
+/* rules_flags bits (RULES.md) */
+#define MTAZ_RF_DOUBLE_STEP 0x1u
+#define MTAZ_RF_PROMO_ALL 0x2u
+#define MTAZ_RF_INSUFFICIENT 0x4u
+#define MTAZ_RF_FIVEFOLD 0x8u
+#define MTAZ_RF_SEVENTYFIVE 0x10u
+#define MTAZ_RF_DEFAULT 0x1Eu
+
+/* ---- library -------------------------------------------------------------------- */
+int mtaz_abi_version(void);
+const char* mtaz_version(void);
+const char* mtaz_last_error(void);
+/* Load the 554-code action space.  Replaces the MOVES_DICT / MOVES_DICT_INV load of
+ * exp/environment.py:15-20 (same JSON file format as exp/moves_dict.json). */
+int mtaz_load_codec(const char* moves_dict_json_path);
+
+/* ---- single-position rules on the host (MinitChessEpisode, exp/environment.py:22-85) */
+int mtaz_pos_from_fen(const char* fen, uint32_t pos[5]);           /* chess.Board(fen)    :25 */
+int mtaz_pos_to_fen(const uint32_t pos[5], char* buf, int cap);    /* Board.fen()         :36 */
+/* sorted legal codes, duplicates kept (exp/environment.py:48-50); returns k */
+int mtaz_pos_legal(const uint32_t pos[5], uint32_t rules_flags, uint16_t* codes, int cap);
+/* Board.result() mapped as exp/environment.py:39-45: 0 ongoing, 1 decisive, 2 draw.
+ * reps = occurrences of the position in the game history (1 without history). */
+int mtaz_pos_outcome(const uint32_t pos[5], uint32_t rules_flags, int move_cap, int reps);
+/* MinitChessEpisode.step(action) (exp/environment.py:68-82): decode, queen retry, push */
+int mtaz_pos_step(const uint32_t pos[5], int code, uint32_t rules_flags, uint32_t out[5]);
+/* 1 if the move of `code` is a capture or a pawn move (python-chess is_zeroing) */
+int mtaz_pos_zeroing(const uint32_t pos[5], int code);
+/* Network.process_observation (exp/policy.py:96-105): 60 tokens + clock */
+int mtaz_pos_encode(const uint32_t pos[5], uint8_t tokens[60], float* clock);
+
+/* ---- numpy legacy RandomState (np.random.* at exp/agent.py:82,115,118) ----------------- */
+size_t mtaz_rng_state_size(void);
+void mtaz_rng_seed(void* state, uint32_t seed);                         /* np.random.seed(s) */
+double mtaz_rng_double(void* state);                                   /* random_sample()   */
+void mtaz_rng_dirichlet(void* state, double alpha, int k, double* out); /* dirichlet([a]*k)  */
+int64_t mtaz_rng_choice_p(void* state, const double* p, int k);        /* choice(k, p=p)    */
+int64_t mtaz_rng_randint(void* state, int64_t m);                      /* choice(m)         */
+
+/* ---- batched device kernels (minimum slice) ------------------------------------------- */
+/* Per position: sorted legal codes (KMAX=256 per row), count, 554-bit mask (18 words),
+ * outcome.  Replaces MinitChessEpisode._update_attributes (exp/environment.py:34-50). */
+int mtaz_legal_batch(int device, const uint32_t* d_pos, int n, uint32_t rules_flags, int move_cap, uint16_t* d_codes,
+                     int32_t* d_counts, uint32_t* d_masks, int32_t* d_outcomes, void* stream);
+/* Network.process_observation for a batch (exp/policy.py:96-105) */
+int mtaz_encode_batch(int device, const uint32_t* d_pos, int n, uint8_t* d_tokens, float* d_clocks, void* stream);
+
+/* ---- engine ------------------------------------------------------------------------- */
+typedef struct mtaz_engine mtaz_engine;
+
+/* One engine per GPU.  Holds n_games game slots, two MCTS tables per slot (the two
+ * SimpleAlphaZeroAgents of app/base.py:113), numpy-legacy RNG per slot seeded
+ * seed_base + slot, and the network.  Replaces SimulatePuppet's agents/env/policy
+ * construction (app/base.py:74-84, :113-114).  numpy_cast_mode: 2 = numpy>=2 promotion
+ * (NEP 50), 1 = numpy 1.x.  NULL on failure. */
+mtaz_engine* mtaz_create(int device, int n_games, int sims, double cpuct, int tau_change, double dir_alpha,
+                         double dir_eps, uint64_t seed_base, int numpy_cast_mode, uint32_t rules_flags, int move_cap);
+void mtaz_destroy(mtaz_engine* h);
+/* SimulatePuppet.load_weights (app/base.py:126-129): the 133 float32 device tensors of
+ * Network.state_dict() in order, num_batches_tracked skipped.  BN is folded and conv
+ * weights re-laid out into engine-owned HBM; the caller's tensors are not retained. */
+int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, const int64_t* numels, int n);
+/* Network.forward (exp/policy.py:71-80) on n device positions: logits [n][554], values [n]. */
+int mtaz_evaluate(mtaz_engine* h, const uint32_t* d_pos, int n, float* d_logits, float* d_values);
+
+/* Batched self-play: n_games full episodes from STARTING_FEN (or the roots set by
+ * mtaz_set_games when from_current != 0).  Replaces erlyx.run_episodes under
+ * SimulatePuppet.run_episodes (app/base.py:108-124). */
+int mtaz_play(mtaz_engine* h, int n_games, int from_current);
+/* Episode records (exp/callbacks.py:31-54 InfoRecorder): per game the ply count; per
+ * ply the observation position, action, legal list length, then the legal codes and
+ * root visit counts N (pi = N / sum N) concatenated over plies. */
+int mtaz_records_counts(mtaz_engine* h, int32_t* plies_per_game, int64_t* total_plies, int64_t* total_entries);
+int mtaz_records_get(mtaz_engine* h, uint32_t* pos, int32_t* action, int32_t* k, uint16_t* codes, uint32_t* visits,
+                     float* reward, int32_t* outcome);
+/* counters of the last mtaz_play: see minitchess_alphazero_amd/engine.py STAT_NAMES */
+int mtaz_stats(mtaz_engine* h, double* out, int n);
+/* record per-wave trunk (18 conv launches) HIP events during mtaz_play */
+int mtaz_set_timing(mtaz_engine* h, int on);
+
+/* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
+ *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */
+int mtaz_set_games(mtaz_engine* h, const uint32_t* roots, const int32_t* agents, const uint8_t* active, int n);
+int mtaz_get_games(mtaz_engine* h, uint32_t* roots, int32_t* agents, uint8_t* active, int32_t* outcome);
+/* MonteCarloInit.on_episode_begin -> agent.init_mcts() (exp/callbacks.py:61-62): tree = 2*game + agent */
+int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n);
+/* root legal count and "root not yet visited" per game (decides the Dirichlet draws) */
+int mtaz_move_begin(mtaz_engine* h, int32_t* root_k, int32_t* root_new);
+/* Dirichlet vectors for this move: game g, draw j, child c at noise[offsets[g] + j*k + c] */
+int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, int64_t total);
+/* run sims [first, first+n) with the GPU network as leaf evaluator */
+int mtaz_simulate(mtaz_engine* h, int first_sim, int n_sims);
+/* host-evaluator mode: select -> (get leaves, caller computes P and v) -> set -> backup */
+int mtaz_sim_select(mtaz_engine* h, int sim);
+int mtaz_leaves_get(mtaz_engine* h, int32_t* count, uint32_t* pos, int32_t* game, int32_t* k, uint16_t* codes);
+int mtaz_leaves_set(mtaz_engine* h, const float* P, const float* v, int count);
+int mtaz_sim_backup(mtaz_engine* h);
+/* root children codes and visit counts [n_games][kout] */
+int mtaz_move_end(mtaz_engine* h, uint16_t* codes, uint32_t* visits, int32_t* k, int kout);
+/* MinitChessEpisode.step for every active game + game-level result (with history) */
+int mtaz_apply(mtaz_engine* h, const int32_t* actions);
+/* read-only tree view for parity tests (mcts['N'|'Q'|'P'|'legal_moves'|'terminal']) */
+int mtaz_tree_size(mtaz_engine* h, int tree, int32_t* nodes, int32_t* edges);
+int mtaz_tree_get(mtaz_engine* h, int tree, uint32_t* pos, uint32_t* e0, uint16_t* k, uint8_t* term, double* tval,
+                  uint16_t* codes, float* P, double* Q, uint32_t* N);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTAZ_H */

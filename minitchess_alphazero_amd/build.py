@@ -1,0 +1,70 @@
+"""Build libmtaz.so (HIP for gfx950) in-tree with hipcc.
+
+Two translation units: csrc/mtaz_device.hip (all kernels + launchers) and
+csrc/mtaz_host.cpp (C ABI, numpy-legacy RNG compiled with -ffp-contract=off,
+engine driver).  The shared object lands next to this file so it travels to the
+GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+OUT = os.path.join(HERE, 'libmtaz.so')
+BUILD = os.path.join(HERE, '_build')
+INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
+ARCH = os.environ.get('MTAZ_OFFLOAD_ARCH', 'gfx950')
+
+SOURCES = [
+    ('mtaz_device.hip', ['-O3']),
+    ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
+]
+HEADERS = ['rules.h', 'engine.h']
+
+
+def _hipcc():
+    for c in ('/opt/rocm/bin/hipcc', 'hipcc'):
+        if os.path.exists(c) or c == 'hipcc':
+            return c
+
+
+def _stale():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, s) for s, _ in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps.append(os.path.join(INCLUDE, 'mtaz.h'))
+    deps.append(os.path.abspath(__file__))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=True):
+    if not force and not _stale():
+        return OUT
+    os.makedirs(BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    objs = []
+    procs = []
+    for src, flags in SOURCES:
+        obj = os.path.join(BUILD, src + '.o')
+        cmd = [hipcc, '-x', 'hip', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-c',
+               os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function'] + flags
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise RuntimeError('hipcc failed: ' + ' '.join(cmd))
+    tmp = OUT + '.tmp'
+    cmd = [hipcc, '-shared', f'--offload-arch={ARCH}', '-o', tmp] + objs + ['-lpthread']
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == '__main__':
+    build(force='--force' in sys.argv)

@@ -1,0 +1,147 @@
+// Engine state shared between the device TU (mtaz_device.hip) and the host TU
+// (mtaz_host.cpp).  All per-game / per-tree state lives in HBM as SoA arrays.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rules.h"
+
+namespace mtaz {
+
+// Action codec (exp/moves_dict.json; SURVEY a-6).  enc[side][from*30+to] -> code
+// or -1; dec[side][code] -> from | to << 8.  side 0 = white, 1 = black.
+struct Codec {
+  int16_t enc[2][900];
+  uint16_t dec[2][NUM_ACTIONS];
+};
+
+constexpr int KMAX = 256;              // max legal-list length handled (error beyond)
+constexpr int MASK_WORDS = 18;         // 554-bit legal mask padded to 576 bits
+constexpr uint32_t NONE = 0xffffffffu;
+
+enum ErrBits : int32_t {
+  ERR_NODES = 1, ERR_EDGES = 2, ERR_DEPTH = 4, ERR_KMAX = 8, ERR_SQRT = 16, ERR_ROOT = 32,
+  ERR_ILLEGAL = 64, ERR_HIST = 128, ERR_HASH = 256,
+};
+
+// MCTS transposition DAG per (game, agent): exp/agent.py:29-36 keeps
+// {Q, N, P, terminal, visited, legal_moves} keyed by FEN; here a node is the
+// packed Pos key in an open-addressing table, its children a contiguous edge
+// range (SoA: code u16, P f32, Q f64, N u32).  Tree t owns nodes [t*NC, (t+1)*NC),
+// hash slots [t*HC, ...), edges [t*EC, ...).
+struct Trees {
+  Pos* node_pos;
+  uint32_t* node_e0;      // tree-local first edge
+  uint16_t* node_k;       // number of children (legal list length, duplicates kept)
+  uint8_t* node_term;     // 1 = terminal (exp/agent.py:59-63)
+  double* node_tval;      // stored terminal value (= -reward)
+  uint32_t* node_sumN;    // sum of child N (exact; numpy N.sum())
+  uint32_t* hash;         // node index + 1, 0 = empty
+  uint32_t* n_nodes;      // [T]
+  uint32_t* n_edges;      // [T]
+  uint16_t* e_code;
+  float* e_P;
+  double* e_Q;
+  uint32_t* e_N;
+  int NC, HC, EC;
+};
+
+struct Games {
+  Pos* root;              // current game position = MCTS root
+  int32_t* agent;         // tree slot (0/1) of the agent to move
+  uint8_t* active;        // 1 while the game runs
+  int32_t* outcome;       // game result (Outcome)
+  int32_t* root_new;      // root absent from the agent's table at move start
+  int32_t* root_k;        // legal-list length of the root
+  int64_t* noise_off;     // this move's Dirichlet vectors: noise[noise_off[g] + j*k + c]
+  double* noise;
+  uint32_t* path_node;    // [G*DMAX] chain of (node, edge) of the current sim
+  uint32_t* path_edge;
+  int32_t* path_len;
+  Pos* hist;              // [G*HMAX] game positions before each move (repetition)
+  int32_t* nhist;
+  int DMAX, HMAX;
+};
+
+struct Leaves {
+  int32_t* count;         // [1]
+  int32_t* game;          // [G]
+  int32_t* tree;          // [G]
+  uint32_t* node;         // [G]
+  Pos* pos;               // [G]
+  float* P;               // [G*KMAX] priors (softmax over the legal logits)
+  float* v;               // [G]
+};
+
+struct Params {
+  int G, sims;
+  float cpuct_f;
+  double cpuct;
+  int cast_mode;          // 2 = numpy>=2 promotion, 1 = numpy 1.x value-based casting
+  uint32_t flags;
+  int move_cap;
+  const double* sqrt_tab; // sqrt(n) for n < sqrt_n (exactly what np.sqrt returns)
+  int sqrt_n;
+  int32_t* err;
+};
+
+struct Dev {
+  Trees tr;
+  Games gm;
+  Leaves lf;
+  Params pr;
+};
+
+// ---- network -------------------------------------------------------------------------
+// Packed weights (BN folded, eval mode).  Conv 3x3 weights are pre-swizzled into the
+// B-fragment order of v_mfma_f32_32x32x2_f32: [cotile 8][kstep/4 288][lane 64][4],
+// kstep s covers k = 2s, 2s+1 with k = tap*256 + ci.
+struct NetWeights {
+  const float* emb;       // [7][4]
+  const float* stem_w;    // [256][72]  (ci*9 + tap), BN folded
+  const float* stem_b;    // [256]
+  const float* conv_w;    // [18][8*288*64*4]
+  const float* conv_b;    // [18][256]
+  const float* pconv_w;   // [2][256] folded
+  const float* pconv_b;   // [2]
+  const float* plin_w;    // [554][61]
+  const float* plin_b;    // [554]
+  const float* vconv_w;   // [256]
+  const float* vconv_b;   // [1]
+  const float* vl1_w;     // [256][31]
+  const float* vl1_b;     // [256]
+  const float* vl2_w;     // [256]
+  const float* vl2_b;     // [1]
+};
+constexpr int CONV_LAYERS = 18;
+constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
+
+struct NetBuffers {
+  float* x0;              // [B][256][32]
+  float* x1;
+  float* t;
+  float* logits;          // [B][554] (evaluate mode only)
+  int B;
+};
+
+// ---- launchers (defined in mtaz_device.hip) ------------------------------------------------
+int dev_upload_codec(const Codec& c);
+void launch_legal_batch(const Pos* pos, int n, uint32_t flags, int move_cap, uint16_t* codes, int32_t* counts,
+                        uint32_t* masks, int32_t* outcomes, hipStream_t s);
+void launch_encode_batch(const Pos* pos, int n, uint8_t* tokens, float* clocks, hipStream_t s);
+void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s);
+void launch_move_begin(const Dev& d, hipStream_t s);
+void launch_select(const Dev& d, int sim, hipStream_t s);
+void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const Pos* pos, const int32_t* count, int max_b,
+                int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end);
+void launch_backup(const Dev& d, hipStream_t s);
+void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
+void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);
+void launch_gather_leaf_codes(const Dev& d, uint16_t* codes_out, int32_t* k_out, hipStream_t s);
+void launch_tree_dump(const Dev& d, int tree, Pos* pos, uint32_t* e0, uint16_t* k, uint8_t* term, double* tval,
+                      uint32_t* sumN, hipStream_t s);
+
+// net modes
+enum NetMode { NET_LEAVES = 0, NET_FULL_LOGITS = 1 };
+
+}  // namespace mtaz

@@ -1,0 +1,770 @@
+// Device side of the MinitChess AlphaZero self-play engine (gfx950 / MI355X).
+//
+//   * rules kernels      batched legal-list / 554-bit mask / outcome / encoder
+//                        (exp/environment.py:34-50, exp/policy.py:82-105)
+//   * MCTS kernels       one wavefront per game: transposition-table lookup, PUCT
+//                        over the children with a wave-wide first-index argmax,
+//                        expansion, terminal handling, backup (exp/agent.py:41-88)
+//   * network kernels    embedding+stem, 18 residual 3x3 convs on fp32 MFMA
+//                        (v_mfma_f32_32x32x2_f32, exact f32 products), fused heads
+//                        with a legal-only softmax (exp/policy.py:71-80, exp/agent.py:67-69)
+#include "engine.h"
+
+namespace mtaz {
+
+static __constant__ Codec d_codec;
+
+int dev_upload_codec(const Codec& c) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(d_codec), &c, sizeof(Codec)) == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------------------
+// wave helpers (64 lanes)
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ BB dev_apply_code(const BB& b, int code) {
+  const int side = b.white ? 0 : 1;
+  const uint16_t ft = d_codec.dec[side][code];
+  const int from = ft & 0xff, to = ft >> 8;
+  // exp/environment.py:71-76: uci4 first, else uci4+'q' -> a pawn reaching the last
+  // rank always promotes to a queen, whichever duplicate code was chosen.
+  const int promo = (((b.pawn >> from) & 1u) && (to / 5 == (b.white ? 5 : 0))) ? QUEEN : 0;
+  return make_move(b, from, to, promo);
+}
+
+// Sorted legal codes with duplicates (exp/environment.py:48-50) computed by one wave:
+// lane s < 30 owns the piece on square s, generates its legal targets, the wave
+// prefix-sums the per-lane counts, scatters the codes to LDS and ranks them.
+// Must be called by all 64 lanes in uniform control flow.  Returns k or -1 (> KMAX).
+__device__ int wave_legal(const BB& b, uint32_t flags, uint16_t* s_raw, uint16_t* s_sorted) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t own = b.white ? b.w : b.b;
+  const int side = b.white ? 0 : 1;
+  uint32_t tg = 0;
+  int cnt = 0;
+  if (lane < NSQ && ((own >> lane) & 1u)) {
+    tg = legal_targets(b, lane, flags);
+    uint32_t m = tg;
+    while (m) {
+      const int to = lsb(m);
+      m &= m - 1;
+      cnt += move_mult(b, lane, to, flags);
+    }
+  }
+  const int incl = wave_incl_scan(cnt);
+  const int total = __shfl(incl, 63, 64);
+  if (total > KMAX) return -1;
+  int off = incl - cnt;
+  uint32_t m = tg;
+  while (m) {
+    const int to = lsb(m);
+    m &= m - 1;
+    const uint16_t code = (uint16_t)d_codec.enc[side][lane * 30 + to];
+    const int mult = move_mult(b, lane, to, flags);
+    for (int r = 0; r < mult; ++r) s_raw[off++] = code;
+  }
+  __syncthreads();
+  for (int j = lane; j < total; j += 64) {
+    const uint16_t c = s_raw[j];
+    int rank = 0;
+    for (int i = 0; i < total; ++i) {
+      const uint16_t o = s_raw[i];
+      rank += (o < c) || (o == c && i < j);
+    }
+    s_sorted[rank] = c;
+  }
+  __syncthreads();
+  return total;
+}
+
+// sequential legal count (one thread), used once per ply at game level
+__device__ int legal_count(const BB& b, uint32_t flags) {
+  const uint32_t own = b.white ? b.w : b.b;
+  uint32_t m = own;
+  int k = 0;
+  while (m) {
+    const int s = lsb(m);
+    m &= m - 1;
+    uint32_t tg = legal_targets(b, s, flags);
+    while (tg) {
+      const int to = lsb(tg);
+      tg &= tg - 1;
+      k += move_mult(b, s, to, flags);
+    }
+  }
+  return k;
+}
+
+// ---------------------------------------------------------------------------------------
+// rules kernels (minimum slice)
+__global__ __launch_bounds__(64) void k_legal_batch(const Pos* __restrict__ pos, int n, uint32_t flags, int move_cap,
+                                                    uint16_t* __restrict__ codes, int32_t* __restrict__ counts,
+                                                    uint32_t* __restrict__ masks, int32_t* __restrict__ outcomes) {
+  __shared__ uint16_t s_raw[KMAX], s_sorted[KMAX];
+  __shared__ uint32_t s_mask[MASK_WORDS];
+  const int i = blockIdx.x, lane = threadIdx.x;
+  if (i >= n) return;
+  const BB b = unpack(pos[i]);
+  if (lane < MASK_WORDS) s_mask[lane] = 0;
+  const int k = wave_legal(b, flags, s_raw, s_sorted);
+  if (k < 0) {
+    if (lane == 0) { counts[i] = -1; outcomes[i] = -1; }
+    return;
+  }
+  for (int j = lane; j < k; j += 64) {
+    codes[(size_t)i * KMAX + j] = s_sorted[j];
+    atomicOr(&s_mask[s_sorted[j] >> 5], 1u << (s_sorted[j] & 31));
+  }
+  __syncthreads();
+  if (lane < MASK_WORDS) masks[(size_t)i * MASK_WORDS + lane] = s_mask[lane];
+  if (lane == 0) {
+    counts[i] = k;
+    outcomes[i] = outcome(b, k, in_check(b), flags, move_cap, 1);
+  }
+}
+
+__global__ void k_encode_batch(const Pos* __restrict__ pos, int n, uint8_t* __restrict__ tokens, float* __restrict__ clocks) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const BB b = unpack(pos[i]);
+  uint8_t t[60];
+  encode_tokens(b, t);
+  for (int j = 0; j < 60; ++j) tokens[(size_t)i * 60 + j] = t[j];
+  clocks[i] = encode_clock(b);
+}
+
+void launch_legal_batch(const Pos* pos, int n, uint32_t flags, int move_cap, uint16_t* codes, int32_t* counts,
+                        uint32_t* masks, int32_t* outcomes, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_legal_batch, dim3(n), dim3(64), 0, s, pos, n, flags, move_cap, codes, counts, masks, outcomes);
+}
+
+void launch_encode_batch(const Pos* pos, int n, uint8_t* tokens, float* clocks, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_encode_batch, dim3((n + 127) / 128), dim3(128), 0, s, pos, n, tokens, clocks);
+}
+
+// ---------------------------------------------------------------------------------------
+// transposition table (open addressing, linear probing; one wave owns a tree at a time)
+__device__ __forceinline__ uint32_t tree_find(const Trees& T, int t, const Pos& p) {
+  const uint32_t mask = (uint32_t)T.HC - 1;
+  const uint32_t* ht = T.hash + (size_t)t * T.HC;
+  const Pos* np = T.node_pos + (size_t)t * T.NC;
+  uint32_t h = pos_hash(p) & mask;
+  for (int probe = 0; probe < T.HC; ++probe) {
+    const uint32_t v = ht[h];
+    if (v == 0) return NONE;
+    if (pos_eq(np[v - 1], p)) return v - 1;
+    h = (h + 1) & mask;
+  }
+  return NONE;
+}
+
+// single lane
+__device__ uint32_t tree_insert(const Trees& T, int t, const Pos& p, int32_t* err) {
+  const uint32_t n = T.n_nodes[t];
+  if (n >= (uint32_t)T.NC) {
+    atomicOr(err, ERR_NODES);
+    return NONE;
+  }
+  T.n_nodes[t] = n + 1;
+  T.node_pos[(size_t)t * T.NC + n] = p;
+  const uint32_t mask = (uint32_t)T.HC - 1;
+  uint32_t* ht = T.hash + (size_t)t * T.HC;
+  uint32_t h = pos_hash(p) & mask;
+  for (int probe = 0; probe < T.HC; ++probe) {
+    if (ht[h] == 0) {
+      ht[h] = n + 1;
+      return n;
+    }
+    h = (h + 1) & mask;
+  }
+  atomicOr(err, ERR_HASH);
+  return NONE;
+}
+
+// exp/agent.py:47-52, one lane: for (node, a) in reversed(chain): value = -value;
+// Q[a] = (N[a]*Q[a] + value) / (N[a] + 1); N[a] += 1.  Exact fp64, no contraction.
+__device__ void backup_path(const Trees& T, int t, const uint32_t* pn, const uint32_t* pe, int depth, double v) {
+#pragma clang fp contract(off)
+  const size_t eb = (size_t)t * T.EC, nbase = (size_t)t * T.NC;
+  for (int d = depth - 1; d >= 0; --d) {
+    v = -v;
+    const size_t e = eb + pe[d];
+    const double N = (double)T.e_N[e];
+    const double Q = T.e_Q[e];
+    const double prod = N * Q;
+    const double num = prod + v;
+    T.e_Q[e] = num / (N + 1.0);
+    T.e_N[e] += 1;
+    T.node_sumN[nbase + pn[d]] += 1;
+  }
+}
+
+__global__ void k_reset_trees(Trees T, const int32_t* __restrict__ trees, int ntrees) {
+  const int j = blockIdx.y;
+  if (j >= ntrees) return;
+  const int t = trees[j];
+  uint32_t* ht = T.hash + (size_t)t * T.HC;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < T.HC; i += gridDim.x * blockDim.x) ht[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    T.n_nodes[t] = 0;
+    T.n_edges[t] = 0;
+  }
+}
+
+void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s) {
+  if (ntrees <= 0) return;
+  hipLaunchKernelGGL(k_reset_trees, dim3(4, ntrees), dim3(256), 0, s, d.tr, trees, ntrees);
+}
+
+// Move start: does the agent's table already hold the root (exp/agent.py:57)?  The host
+// needs k and "root is new" to draw exactly sims - root_new Dirichlet vectors (:81-82).
+__global__ __launch_bounds__(64) void k_move_begin(Dev D) {
+  __shared__ uint16_t s_raw[KMAX], s_sorted[KMAX];
+  const int g = blockIdx.x, lane = threadIdx.x;
+  if (!D.gm.active[g]) {
+    if (lane == 0) { D.gm.root_k[g] = 0; D.gm.root_new[g] = 0; }
+    return;
+  }
+  const int t = 2 * g + D.gm.agent[g];
+  const Pos root = D.gm.root[g];
+  const uint32_t n = tree_find(D.tr, t, root);
+  if (n != NONE) {
+    if (lane == 0) {
+      if (D.tr.node_term[(size_t)t * D.tr.NC + n]) atomicOr(D.pr.err, ERR_ROOT);
+      D.gm.root_k[g] = D.tr.node_k[(size_t)t * D.tr.NC + n];
+      D.gm.root_new[g] = 0;
+    }
+    return;
+  }
+  const BB b = unpack(root);
+  const int k = wave_legal(b, D.pr.flags, s_raw, s_sorted);
+  if (lane == 0) {
+    if (k <= 0) atomicOr(D.pr.err, k < 0 ? ERR_KMAX : ERR_ROOT);
+    D.gm.root_k[g] = k;
+    D.gm.root_new[g] = 1;
+  }
+}
+
+void launch_move_begin(const Dev& d, hipStream_t s) {
+  hipLaunchKernelGGL(k_move_begin, dim3(d.pr.G), dim3(64), 0, s, d);
+}
+
+// One simulation for every active game (exp/agent.py:41-88): descend from the root by
+// PUCT until an unvisited node (expand: terminal -> back up, else queue the leaf for
+// the network) or a stored terminal (back up -terminal, the reference's sign quirk).
+__global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
+#pragma clang fp contract(off)
+  __shared__ uint16_t s_raw[KMAX], s_sorted[KMAX];
+  const int g = blockIdx.x, lane = threadIdx.x;
+  if (!D.gm.active[g]) return;
+  const Trees& T = D.tr;
+  const int t = 2 * g + D.gm.agent[g];
+  const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
+  uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
+  uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
+  Pos pos = D.gm.root[g];
+  int depth = 0;
+  for (;;) {
+    const uint32_t n = tree_find(T, t, pos);
+    if (n == NONE) {
+      // ---- expansion (exp/agent.py:57-73) ----
+      const BB b = unpack(pos);
+      const int k = wave_legal(b, D.pr.flags, s_raw, s_sorted);
+      if (k < 0) {
+        if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
+        return;
+      }
+      const int oc = outcome(b, k, in_check(b), D.pr.flags, D.pr.move_cap, 1);
+      uint32_t nn = NONE, e0 = 0;
+      if (lane == 0) {
+        nn = tree_insert(T, t, pos, D.pr.err);
+        if (nn != NONE) {
+          if (oc != ONGOING) {
+            const double value = (oc == DECISIVE) ? -1.0 : -0.0;   // -reward
+            T.node_term[nbase + nn] = 1;
+            T.node_tval[nbase + nn] = value;
+            T.node_k[nbase + nn] = 0;
+            T.node_e0[nbase + nn] = 0;
+            T.node_sumN[nbase + nn] = 0;
+            backup_path(T, t, pn, pe, depth, value);
+          } else {
+            e0 = T.n_edges[t];
+            if (e0 + (uint32_t)k > (uint32_t)T.EC) {
+              atomicOr(D.pr.err, ERR_EDGES);
+              nn = NONE;
+            } else {
+              T.n_edges[t] = e0 + k;
+              T.node_term[nbase + nn] = 0;
+              T.node_k[nbase + nn] = (uint16_t)k;
+              T.node_e0[nbase + nn] = e0;
+              T.node_sumN[nbase + nn] = 0;
+              const int slot = atomicAdd(D.lf.count, 1);
+              D.lf.game[slot] = g;
+              D.lf.tree[slot] = t;
+              D.lf.node[slot] = nn;
+              D.lf.pos[slot] = pos;
+              D.gm.path_len[g] = depth;
+            }
+          }
+        }
+      }
+      nn = __shfl(nn, 0, 64);
+      e0 = __shfl(e0, 0, 64);
+      if (oc == ONGOING && nn != NONE) {
+        for (int c = lane; c < k; c += 64) {
+          T.e_code[ebase + e0 + c] = s_sorted[c];
+          T.e_P[ebase + e0 + c] = 0.f;
+          T.e_Q[ebase + e0 + c] = 0.0;
+          T.e_N[ebase + e0 + c] = 0;
+        }
+      }
+      return;
+    }
+    if (T.node_term[nbase + n]) {
+      if (lane == 0) backup_path(T, t, pn, pe, depth, -T.node_tval[nbase + n]);
+      return;
+    }
+    // ---- selection (exp/agent.py:79-85) ----
+    const uint32_t e0 = T.node_e0[nbase + n];
+    const int k = T.node_k[nbase + n];
+    const uint32_t S = T.node_sumN[nbase + n];
+    if (S >= (uint32_t)D.pr.sqrt_n) {
+      if (lane == 0) atomicOr(D.pr.err, ERR_SQRT);
+      return;
+    }
+    const double sq = D.pr.sqrt_tab[S];
+    const bool root = depth == 0;
+    const double* noise = nullptr;
+    if (root) {
+      const int j = sim - D.gm.root_new[g];
+      noise = D.gm.noise + D.gm.noise_off[g] + (int64_t)j * k;
+    }
+    double best_u = -__builtin_inf();
+    int best_i = 0x7fffffff;
+    for (int c = lane; c < k; c += 64) {
+      const size_t e = ebase + e0 + c;
+      const float Pf = T.e_P[e];
+      const double Q = T.e_Q[e];
+      const double N = (double)T.e_N[e];
+      double tt;
+      if (root) {
+        // P = 0.75*P (float32) + 0.25*dirichlet (float64)  -> float64
+        const float p75 = 0.75f * Pf;
+        const double pp = (double)p75 + 0.25 * noise[c];
+        tt = (D.pr.cpuct * pp) * sq;
+      } else if (D.pr.cast_mode == 2) {
+        const float cp = D.pr.cpuct_f * Pf;       // float32 array * python scalar
+        tt = (double)cp * sq;                     // * np.float64 scalar -> float64 (NEP 50)
+      } else {
+        const float cp = D.pr.cpuct_f * Pf;
+        tt = (double)(cp * (float)sq);            // numpy 1.x: stays float32
+      }
+      const double u = Q + tt / (1.0 + N);
+      if (u > best_u) { best_u = u; best_i = c; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ou = __shfl_xor(best_u, o, 64);
+      const int oi = __shfl_xor(best_i, o, 64);
+      if (ou > best_u || (ou == best_u && oi < best_i)) { best_u = ou; best_i = oi; }
+    }
+    const int a = best_i;
+    if (depth >= D.gm.DMAX) {
+      if (lane == 0) atomicOr(D.pr.err, ERR_DEPTH);
+      return;
+    }
+    if (lane == 0) {
+      pn[depth] = n;
+      pe[depth] = e0 + a;
+    }
+    ++depth;
+    const int code = T.e_code[ebase + e0 + a];
+    pos = pack(dev_apply_code(unpack(pos), code));
+  }
+}
+
+void launch_select(const Dev& d, int sim, hipStream_t s) {
+  hipLaunchKernelGGL(k_select, dim3(d.pr.G), dim3(64), 0, s, d, sim);
+}
+
+// Leaf expansion finish + backup (exp/agent.py:68-72): store P, back up v.
+__global__ void k_backup(Dev D) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *D.lf.count) return;
+  const Trees& T = D.tr;
+  const int g = D.lf.game[i], t = D.lf.tree[i];
+  const uint32_t n = D.lf.node[i];
+  const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
+  const int k = T.node_k[nbase + n];
+  const uint32_t e0 = T.node_e0[nbase + n];
+  for (int c = 0; c < k; ++c) T.e_P[ebase + e0 + c] = D.lf.P[(size_t)i * KMAX + c];
+  const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
+  const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
+  backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i]);
+}
+
+void launch_backup(const Dev& d, hipStream_t s) {
+  hipLaunchKernelGGL(k_backup, dim3((d.pr.G + 63) / 64), dim3(64), 0, s, d);
+}
+
+__global__ void k_gather_leaf_codes(Dev D, uint16_t* __restrict__ codes, int32_t* __restrict__ kout) {
+  const int i = blockIdx.x;
+  if (i >= *D.lf.count) return;
+  const Trees& T = D.tr;
+  const int t = D.lf.tree[i];
+  const uint32_t n = D.lf.node[i];
+  const int k = T.node_k[(size_t)t * T.NC + n];
+  const uint32_t e0 = T.node_e0[(size_t)t * T.NC + n];
+  for (int c = threadIdx.x; c < k; c += blockDim.x) codes[(size_t)i * KMAX + c] = T.e_code[(size_t)t * T.EC + e0 + c];
+  if (threadIdx.x == 0) kout[i] = k;
+}
+
+void launch_gather_leaf_codes(const Dev& d, uint16_t* codes_out, int32_t* k_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_leaf_codes, dim3(d.pr.G), dim3(64), 0, s, d, codes_out, k_out);
+}
+
+// Root visit counts after the search (exp/policy.py:119-121: pi = N / N.sum()).
+__global__ __launch_bounds__(64) void k_move_end(Dev D, uint16_t* __restrict__ codes, uint32_t* __restrict__ visits, int kout) {
+  const int g = blockIdx.x, lane = threadIdx.x;
+  if (!D.gm.active[g]) return;
+  const Trees& T = D.tr;
+  const int t = 2 * g + D.gm.agent[g];
+  const uint32_t n = tree_find(T, t, D.gm.root[g]);
+  if (n == NONE) {
+    if (lane == 0) atomicOr(D.pr.err, ERR_ROOT);
+    return;
+  }
+  const int k = T.node_k[(size_t)t * T.NC + n];
+  const uint32_t e0 = T.node_e0[(size_t)t * T.NC + n];
+  if (k > kout) {
+    if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
+    return;
+  }
+  for (int c = lane; c < k; c += 64) {
+    codes[(size_t)g * kout + c] = T.e_code[(size_t)t * T.EC + e0 + c];
+    visits[(size_t)g * kout + c] = T.e_N[(size_t)t * T.EC + e0 + c];
+  }
+}
+
+void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s) {
+  hipLaunchKernelGGL(k_move_end, dim3(d.pr.G), dim3(64), 0, s, d, codes_out, visits_out, kout);
+}
+
+// Game step (exp/environment.py:68-82) + game-level result with history (fivefold
+// repetition compares the positions since the last zeroing move).
+__global__ void k_apply(Dev D, const int32_t* __restrict__ actions) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= D.pr.G || !D.gm.active[g]) return;
+  const Pos p = D.gm.root[g];
+  const BB b = unpack(p);
+  const int code = actions[g];
+  bool ok = code >= 0 && code < NUM_ACTIONS;
+  int from = 0, to = 0;
+  if (ok) {
+    const uint16_t ft = d_codec.dec[b.white ? 0 : 1][code];
+    from = ft & 0xff;
+    to = ft >> 8;
+    const uint32_t own = b.white ? b.w : b.b;
+    ok = ((own >> from) & 1u) && ((legal_targets(b, from, D.pr.flags) >> to) & 1u);
+  }
+  const int nh = D.gm.nhist[g];
+  if (!ok || nh >= D.gm.HMAX) {
+    atomicOr(D.pr.err, ok ? ERR_HIST : ERR_ILLEGAL);
+    D.gm.active[g] = 0;
+    D.gm.outcome[g] = -1;
+    return;
+  }
+  Pos* hist = D.gm.hist + (size_t)g * D.gm.HMAX;
+  hist[nh] = p;
+  const BB nb = dev_apply_code(b, code);
+  const Pos np = pack(nb);
+  int reps = 1;
+  for (int i = nh; i >= 0 && i > nh - nb.half; --i)
+    if (pos_eq_board_turn(hist[i], np)) ++reps;
+  const int k = legal_count(nb, D.pr.flags);
+  const int oc = outcome(nb, k, in_check(nb), D.pr.flags, D.pr.move_cap, reps);
+  D.gm.root[g] = np;
+  D.gm.agent[g] ^= 1;
+  D.gm.nhist[g] = nh + 1;
+  D.gm.outcome[g] = oc;
+  if (oc != ONGOING) D.gm.active[g] = 0;
+}
+
+void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s) {
+  hipLaunchKernelGGL(k_apply, dim3((d.pr.G + 127) / 128), dim3(128), 0, s, d, actions);
+}
+
+// ---------------------------------------------------------------------------------------
+// network
+__device__ __forceinline__ int padpos(int p) { return (p / 5 + 1) * 7 + (p % 5 + 1); }   // 8x7 zero-padded board
+
+// Embedding(7,4) -> permute -> (8, 6, 5) -> Conv3x3(8->256)+BN+ReLU (exp/policy.py:58, :72-73).
+// One 256-thread block per board, thread = output channel.
+__global__ __launch_bounds__(256) void k_stem(const Pos* __restrict__ pos, const int32_t* __restrict__ count, int max_b,
+                                              NetWeights W, float* __restrict__ out) {
+  __shared__ float xin[8 * 56];
+  __shared__ uint8_t tok[60];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nb = count ? *count : max_b;
+  if (b >= nb) return;
+  for (int i = tid; i < 8 * 56; i += 256) xin[i] = 0.f;
+  if (tid == 0) encode_tokens(unpack(pos[b]), tok);
+  __syncthreads();
+  if (tid < 240) {
+    const int c = tid / 30, p = tid % 30;         // c = plane*4 + e
+    xin[c * 56 + padpos(p)] = W.emb[tok[(c >> 2) * 30 + p] * 4 + (c & 3)];
+  }
+  __syncthreads();
+  const int co = tid;
+  float w[72];
+#pragma unroll
+  for (int j = 0; j < 72; ++j) w[j] = W.stem_w[co * 72 + j];
+  const float bias = W.stem_b[co];
+  float* o = out + (size_t)b * 8192 + co * 32;
+  for (int p = 0; p < 30; ++p) {
+    const int pp = padpos(p);
+    float acc = bias;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) acc += w[ci * 9 + tap] * xin[ci * 56 + pp + (tap / 3 - 1) * 7 + (tap % 3 - 1)];
+    o[p] = fmaxf(acc, 0.f);
+  }
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Residual-trunk 3x3 conv (256 -> 256) + folded BN (+ residual) + ReLU as an implicit
+// GEMM on fp32 MFMA: M = board positions (one 32-row tile per board, rows 30/31 are
+// padding), N = output channels, K = 9 taps x 256 input channels = 2304.
+// Block = 256 threads (4 waves) x 2 boards; the two input boards sit in LDS as
+// [ci][board][8x7 padded] fp32 (114,688 B), so the whole K loop runs barrier-free from
+// LDS + L2-resident pre-swizzled weights (one float4 per lane per 4 k-steps).
+// Wave w computes output channels [64w, 64w+64) for both boards: 4 accumulators of
+// 32x32 (v_mfma_f32_32x32x2_f32: lane l holds A[row l&31][k l>>5], B[k l>>5][col l&31]).
+__global__ __launch_bounds__(256, 1) void k_conv3x3(const float* __restrict__ in, const float* __restrict__ resid,
+                                                    float* __restrict__ out, const float4* __restrict__ wpk,
+                                                    const float* __restrict__ bias, const int32_t* __restrict__ count,
+                                                    int max_b) {
+  __shared__ float lds[2 * 256 * 56];
+  const int nb = count ? *count : max_b;
+  const int b0 = blockIdx.x * 2;
+  if (b0 >= nb) return;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * 256 * 56; i += 256) lds[i] = 0.f;
+  __syncthreads();
+  // stage: in[b][ci][0..31] as 8 float4 per (board, ci)
+  for (int idx = tid; idx < 2 * 256 * 8; idx += 256) {
+    const int bb = idx >> 11, rem = idx & 2047, ci = rem >> 3, q = rem & 7;
+    const int b = b0 + bb;
+    if (b < nb) {
+      const float4 v = reinterpret_cast<const float4*>(in + (size_t)b * 8192 + ci * 32)[q];
+      float* dst = lds + (ci * 2 + bb) * 56;
+      const int p0 = q * 4;
+      if (p0 + 0 < 30) dst[padpos(p0 + 0)] = v.x;
+      if (p0 + 1 < 30) dst[padpos(p0 + 1)] = v.y;
+      if (p0 + 2 < 30) dst[padpos(p0 + 2)] = v.z;
+      if (p0 + 3 < 30) dst[padpos(p0 + 3)] = v.w;
+    }
+  }
+  __syncthreads();
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int row = lane & 31, kh = lane >> 5;
+  const int pp = padpos(row < 30 ? row : 29);       // rows 30/31: any valid address, outputs discarded
+  const float4* w0 = wpk + (size_t)(2 * wave) * 288 * 64 + lane;
+  const float4* w1 = wpk + (size_t)(2 * wave + 1) * 288 * 64 + lane;
+  f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  float4 nb0 = w0[0], nb1 = w1[0];
+  for (int tap = 0; tap < 9; ++tap) {
+    const int off = (tap / 3 - 1) * 7 + (tap % 3 - 1);
+    const float* abase = lds + kh * 112 + pp + off;
+    for (int q = 0; q < 32; ++q) {
+      const int s4 = tap * 32 + q;
+      const float4 cb0 = nb0, cb1 = nb1;
+      if (s4 + 1 < 288) {
+        nb0 = w0[(s4 + 1) * 64];
+        nb1 = w1[(s4 + 1) * 64];
+      }
+      const float* a = abase + q * 4 * 224;
+      const float a00 = a[0], a01 = a[56];
+      const float a10 = a[224], a11 = a[224 + 56];
+      const float a20 = a[448], a21 = a[448 + 56];
+      const float a30 = a[672], a31 = a[672 + 56];
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a00, cb0.x, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a00, cb1.x, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a01, cb0.x, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a01, cb1.x, acc11, 0, 0, 0);
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a10, cb0.y, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a10, cb1.y, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a11, cb0.y, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a11, cb1.y, acc11, 0, 0, 0);
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a20, cb0.z, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a20, cb1.z, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a21, cb0.z, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a21, cb1.z, acc11, 0, 0, 0);
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a30, cb0.w, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a30, cb1.w, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a31, cb0.w, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a31, cb1.w, acc11, 0, 0, 0);
+    }
+  }
+  // epilogue: col = lane&31 -> channel; rows (r&3) + 8(r>>2) + 4*kh -> positions
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int b = b0 + bb;
+    if (b >= nb) continue;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const f32x16 acc = bb == 0 ? (ct == 0 ? acc00 : acc01) : (ct == 0 ? acc10 : acc11);
+      const int co = (2 * wave + ct) * 32 + row;
+      const float bv = bias[co];
+      const size_t obase = (size_t)b * 8192 + co * 32;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int r0 = 8 * g4 + 4 * kh;
+        float4 v = make_float4(acc[4 * g4 + 0] + bv, acc[4 * g4 + 1] + bv, acc[4 * g4 + 2] + bv, acc[4 * g4 + 3] + bv);
+        if (resid) {
+          const float4 r = *reinterpret_cast<const float4*>(resid + obase + r0);
+          v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+        }
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        *reinterpret_cast<float4*>(out + obase + r0) = v;
+      }
+    }
+  }
+}
+
+// Heads (exp/policy.py:62-69, :76-79) + leaf prior extraction (exp/agent.py:67-69):
+// pconv/vconv 1x1 + BN + ReLU, value MLP + tanh, policy logits for the legal codes only
+// and a float32 softmax over them (duplicates included).  One block per board.
+__global__ __launch_bounds__(256) void k_heads(Dev D, NetWeights W, const float* __restrict__ x, const Pos* __restrict__ pos,
+                                               const int32_t* __restrict__ count, int max_b, int mode,
+                                               float* __restrict__ logits_out, float* __restrict__ values_out) {
+  __shared__ float xs[256 * 31];
+  __shared__ float fp[64], fv[32];
+  __shared__ float red[256];
+  __shared__ float sl[KMAX];
+  __shared__ uint16_t scode[KMAX];
+  __shared__ int sk;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nb = count ? *count : max_b;
+  if (b >= nb) return;
+  for (int idx = tid; idx < 256 * 30; idx += 256) {
+    const int c = idx / 30, p = idx - c * 30;
+    xs[c * 31 + p] = x[(size_t)b * 8192 + c * 32 + p];
+  }
+  if (tid == 0) {
+    const BB bb = unpack(pos[b]);
+    const float clk = encode_clock(bb);
+    fp[60] = clk;
+    fv[30] = clk;
+  }
+  if (mode == NET_LEAVES && tid == 0) {
+    const int t = D.lf.tree[b];
+    const uint32_t n = D.lf.node[b];
+    sk = D.tr.node_k[(size_t)t * D.tr.NC + n];
+  }
+  __syncthreads();
+  if (mode == NET_LEAVES) {
+    const int t = D.lf.tree[b];
+    const uint32_t n = D.lf.node[b];
+    const uint32_t e0 = D.tr.node_e0[(size_t)t * D.tr.NC + n];
+    for (int c = tid; c < sk; c += 256) scode[c] = D.tr.e_code[(size_t)t * D.tr.EC + e0 + c];
+  }
+  if (tid < 90) {
+    const int o = tid / 30, p = tid - o * 30;
+    const float* wr = o < 2 ? W.pconv_w + o * 256 : W.vconv_w;
+    float s = 0.f;
+    for (int c = 0; c < 256; ++c) s += wr[c] * xs[c * 31 + p];
+    s += o < 2 ? W.pconv_b[o] : W.vconv_b[0];
+    s = fmaxf(s, 0.f);
+    if (o < 2) fp[o * 30 + p] = s; else fv[p] = s;
+  }
+  __syncthreads();
+  // value: Linear(31,256) ReLU Linear(256,1) Tanh
+  {
+    float h = W.vl1_b[tid];
+    for (int i = 0; i < 31; ++i) h += W.vl1_w[tid * 31 + i] * fv[i];
+    h = fmaxf(h, 0.f);
+    red[tid] = W.vl2_w[tid] * h;
+  }
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float v = tanhf(red[0] + W.vl2_b[0]);
+    if (mode == NET_LEAVES) D.lf.v[b] = v; else values_out[b] = v;
+  }
+  __syncthreads();
+  if (mode == NET_FULL_LOGITS) {
+    for (int a = tid; a < NUM_ACTIONS; a += 256) {
+      float l = W.plin_b[a];
+      for (int j = 0; j < 61; ++j) l += W.plin_w[a * 61 + j] * fp[j];
+      logits_out[(size_t)b * NUM_ACTIONS + a] = l;
+    }
+    return;
+  }
+  const int k = sk;
+  for (int c = tid; c < k; c += 256) {
+    const int a = scode[c];
+    float l = W.plin_b[a];
+    for (int j = 0; j < 61; ++j) l += W.plin_w[a * 61 + j] * fp[j];
+    sl[c] = l;
+  }
+  __syncthreads();
+  // softmax over the k gathered logits (k <= KMAX = 256: one element per thread)
+  red[tid] = tid < k ? sl[tid] : -__builtin_inff();
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = fmaxf(red[tid], red[tid + s]);
+    __syncthreads();
+  }
+  const float mx = red[0];
+  __syncthreads();
+  const float ex = tid < k ? expf(sl[tid] - mx) : 0.f;
+  red[tid] = ex;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  const float sum = red[0];
+  if (tid < k) D.lf.P[(size_t)b * KMAX + tid] = ex / sum;
+}
+
+void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nbuf, const Pos* pos, const int32_t* count, int max_b,
+                int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end) {
+  if (max_b <= 0) return;
+  hipLaunchKernelGGL(k_stem, dim3(max_b), dim3(256), 0, s, pos, count, max_b, w, nbuf.x0);
+  if (trunk_begin) (void)hipEventRecord(trunk_begin, s);
+  float* xc = nbuf.x0;
+  float* xn = nbuf.x1;
+  const int grid = (max_b + 1) / 2;
+  for (int blk = 0; blk < 9; ++blk) {
+    const int la = 2 * blk, lb = 2 * blk + 1;
+    hipLaunchKernelGGL(k_conv3x3, dim3(grid), dim3(256), 0, s, xc, (const float*)nullptr, nbuf.t,
+                       reinterpret_cast<const float4*>(w.conv_w + la * CONV_W_FLOATS), w.conv_b + la * 256, count, max_b);
+    hipLaunchKernelGGL(k_conv3x3, dim3(grid), dim3(256), 0, s, nbuf.t, (const float*)xc, xn,
+                       reinterpret_cast<const float4*>(w.conv_w + lb * CONV_W_FLOATS), w.conv_b + lb * 256, count, max_b);
+    float* tmp = xc;
+    xc = xn;
+    xn = tmp;
+  }
+  if (trunk_end) (void)hipEventRecord(trunk_end, s);
+  hipLaunchKernelGGL(k_heads, dim3(max_b), dim3(256), 0, s, d, w, xc, pos, count, max_b, mode, nbuf.logits, values_out);
+}
+
+}  // namespace mtaz

@@ -1,0 +1,1159 @@
+// Host side of the mtaz engine: the C ABI of include/mtaz.h.
+//
+//   * codec loader        exp/moves_dict.json format (exp/environment.py:15-20)
+//   * host rules / FEN    single-position MinitChessEpisode support (exp/environment.py:22-85)
+//   * numpy legacy RNG    MT19937 + legacy gamma / dirichlet / choice, bit-exact with
+//                         numpy.random.RandomState (exp/agent.py:82,115,118); compiled
+//                         without FP contraction and calling the same libm log/pow
+//   * engine              HBM allocation, BN folding + MFMA weight swizzle, and the
+//                         batched self-play driver that replaces erlyx.run_episodes
+//                         under SimulatePuppet.run_episodes (app/base.py:108-124)
+#pragma STDC FP_CONTRACT OFF
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mtaz.h"
+#include "engine.h"
+
+using namespace mtaz;
+
+// ---------------------------------------------------------------------------------------
+// errors
+static thread_local std::string g_err;
+static int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIPCHK(x)                                                                            \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) return set_err(MTAZ_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" int mtaz_abi_version(void) { return MTAZ_ABI_VERSION; }
+extern "C" const char* mtaz_version(void) { return "mtaz 0.1 (gfx950)"; }
+extern "C" const char* mtaz_last_error(void) { return g_err.c_str(); }
+
+// ---------------------------------------------------------------------------------------
+// codec
+static Codec h_codec;
+static bool h_codec_ok = false;
+
+static int sq_from_name(const char* s) {
+  if (s[0] < 'a' || s[0] > 'e' || s[1] < '1' || s[1] > '6') return -1;
+  return (s[1] - '1') * 5 + (s[0] - 'a');
+}
+
+// Parses {"w": {"a1b2": 0, ...}, "b": {...}} (json.dump default formatting, or any
+// whitespace).  Every code must appear exactly once per side.
+extern "C" int mtaz_load_codec(const char* path) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return set_err(MTAZ_E_FAIL, "cannot open %s", path);
+  std::string s;
+  char buf[4096];
+  size_t r;
+  while ((r = fread(buf, 1, sizeof(buf), f)) > 0) s.append(buf, r);
+  fclose(f);
+  Codec c;
+  memset(c.enc, 0xff, sizeof(c.enc));
+  memset(c.dec, 0xff, sizeof(c.dec));
+  int side = -1, seen[2] = {0, 0};
+  size_t i = 0;
+  while (i < s.size()) {
+    if (s[i] != '"') { ++i; continue; }
+    const size_t j = s.find('"', i + 1);
+    if (j == std::string::npos) break;
+    const std::string key = s.substr(i + 1, j - i - 1);
+    i = j + 1;
+    if (key == "w" || key == "b") { side = key == "w" ? 0 : 1; continue; }
+    if (key.size() != 4 || side < 0) return set_err(MTAZ_E_FAIL, "codec: unexpected key '%s'", key.c_str());
+    while (i < s.size() && (s[i] == ':' || s[i] == ' ')) ++i;
+    int code = 0, nd = 0;
+    while (i < s.size() && s[i] >= '0' && s[i] <= '9') { code = code * 10 + (s[i] - '0'); ++i; ++nd; }
+    const int from = sq_from_name(key.c_str()), to = sq_from_name(key.c_str() + 2);
+    if (!nd || from < 0 || to < 0 || code >= NUM_ACTIONS) return set_err(MTAZ_E_FAIL, "codec: bad entry '%s'", key.c_str());
+    if (c.dec[side][code] != 0xffff) return set_err(MTAZ_E_FAIL, "codec: duplicate code %d", code);
+    c.enc[side][from * 30 + to] = (int16_t)code;
+    c.dec[side][code] = (uint16_t)(from | (to << 8));
+    ++seen[side];
+  }
+  if (seen[0] != NUM_ACTIONS || seen[1] != NUM_ACTIONS)
+    return set_err(MTAZ_E_FAIL, "codec: expected %d codes per side, got %d/%d", NUM_ACTIONS, seen[0], seen[1]);
+  h_codec = c;
+  h_codec_ok = true;
+  return 0;
+}
+
+static int ensure_codec_device(int device) {
+  if (!h_codec_ok) return set_err(MTAZ_E_FAIL, "codec not loaded (mtaz_load_codec)");
+  HIPCHK(hipSetDevice(device));
+  if (dev_upload_codec(h_codec)) return set_err(MTAZ_E_DEVICE, "codec upload failed");
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// host rules
+static inline Pos pos_in(const uint32_t* p) { Pos x; memcpy(&x, p, sizeof(Pos)); return x; }
+static inline void pos_out(const Pos& x, uint32_t* p) { memcpy(p, &x, sizeof(Pos)); }
+
+static int host_legal(const BB& b, uint32_t flags, uint16_t* out, int cap) {
+  const uint32_t own = b.white ? b.w : b.b;
+  const int side = b.white ? 0 : 1;
+  int k = 0;
+  uint32_t m = own;
+  while (m) {
+    const int s = lsb(m);
+    m &= m - 1;
+    uint32_t tg = legal_targets(b, s, flags);
+    while (tg) {
+      const int to = lsb(tg);
+      tg &= tg - 1;
+      const int code = h_codec.enc[side][s * 30 + to];
+      const int mult = move_mult(b, s, to, flags);
+      for (int r = 0; r < mult; ++r) {
+        if (k >= cap) return -1;
+        out[k++] = (uint16_t)code;
+      }
+    }
+  }
+  std::sort(out, out + k);
+  return k;
+}
+
+static const char* PIECES = ".pnbrqk";
+
+extern "C" int mtaz_pos_from_fen(const char* fen, uint32_t out[5]) {
+  BB b{};
+  int r = 5, f = 0;
+  const char* p = fen;
+  for (; *p && *p != ' '; ++p) {
+    const char ch = *p;
+    if (ch == '/') {
+      if (f != 5) return set_err(MTAZ_E_FAIL, "bad FEN rank in '%s'", fen);
+      --r; f = 0;
+      if (r < 0) return set_err(MTAZ_E_FAIL, "too many ranks in '%s'", fen);
+    } else if (ch >= '1' && ch <= '5') {
+      f += ch - '0';
+    } else {
+      const char lc = (ch >= 'A' && ch <= 'Z') ? ch - 'A' + 'a' : ch;
+      const char* q = strchr(PIECES + 1, lc);
+      if (!q || f >= 5) return set_err(MTAZ_E_FAIL, "bad FEN piece in '%s'", fen);
+      set_piece(b, r * 5 + f, (int)(q - PIECES), ch >= 'A' && ch <= 'Z');
+      ++f;
+    }
+    if (f > 5) return set_err(MTAZ_E_FAIL, "bad FEN rank in '%s'", fen);
+  }
+  if (r != 0 || f != 5) return set_err(MTAZ_E_FAIL, "FEN must have 6 ranks of 5 files: '%s'", fen);
+  char turn = 0;
+  int half = -1, full = -1;
+  if (sscanf(p, " %c %d %d", &turn, &half, &full) != 3 || (turn != 'w' && turn != 'b') || half < 0 || full < 0 ||
+      half > 255 || full > 65535)
+    return set_err(MTAZ_E_FAIL, "expected 4-field MinitChess FEN 'board turn half full': '%s'", fen);
+  b.white = turn == 'w';
+  b.half = half;
+  b.full = full;
+  pos_out(pack(b), out);
+  return 0;
+}
+
+extern "C" int mtaz_pos_to_fen(const uint32_t pos[5], char* buf, int cap) {
+  const BB b = unpack(pos_in(pos));
+  std::string s;
+  for (int r = 5; r >= 0; --r) {
+    int e = 0;
+    for (int f = 0; f < 5; ++f) {
+      const int sq = r * 5 + f, t = piece_type_at(b, sq);
+      if (!t) { ++e; continue; }
+      if (e) { s += (char)('0' + e); e = 0; }
+      char ch = PIECES[t];
+      if ((b.w >> sq) & 1u) ch = ch - 'a' + 'A';
+      s += ch;
+    }
+    if (e) s += (char)('0' + e);
+    if (r) s += '/';
+  }
+  s += b.white ? " w " : " b ";
+  s += std::to_string(b.half) + " " + std::to_string(b.full);
+  if ((int)s.size() + 1 > cap) return set_err(MTAZ_E_CAPACITY, "fen buffer too small");
+  memcpy(buf, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+
+extern "C" int mtaz_pos_legal(const uint32_t pos[5], uint32_t flags, uint16_t* codes, int cap) {
+  if (!h_codec_ok) return set_err(MTAZ_E_FAIL, "codec not loaded");
+  const int k = host_legal(unpack(pos_in(pos)), flags, codes, cap);
+  return k < 0 ? set_err(MTAZ_E_CAPACITY, "legal list longer than %d", cap) : k;
+}
+
+extern "C" int mtaz_pos_outcome(const uint32_t pos[5], uint32_t flags, int move_cap, int reps) {
+  if (!h_codec_ok) return set_err(MTAZ_E_FAIL, "codec not loaded");
+  const BB b = unpack(pos_in(pos));
+  uint16_t tmp[KMAX];
+  const int k = host_legal(b, flags, tmp, KMAX);
+  if (k < 0) return set_err(MTAZ_E_CAPACITY, "legal list too long");
+  return outcome(b, k, in_check(b), flags, move_cap, reps);
+}
+
+static int host_decode(const BB& b, int code, int* from, int* to) {
+  if (code < 0 || code >= NUM_ACTIONS) return -1;
+  const uint16_t ft = h_codec.dec[b.white ? 0 : 1][code];
+  *from = ft & 0xff;
+  *to = ft >> 8;
+  return 0;
+}
+
+extern "C" int mtaz_pos_step(const uint32_t pos[5], int code, uint32_t flags, uint32_t out[5]) {
+  if (!h_codec_ok) return set_err(MTAZ_E_FAIL, "codec not loaded");
+  const BB b = unpack(pos_in(pos));
+  int from, to;
+  if (host_decode(b, code, &from, &to)) return set_err(MTAZ_E_ILLEGAL, "action %d out of range", code);
+  const uint32_t own = b.white ? b.w : b.b;
+  if (!((own >> from) & 1u) || !((legal_targets(b, from, flags) >> to) & 1u))
+    return set_err(MTAZ_E_ILLEGAL, "action %d is not legal", code);
+  const int promo = (((b.pawn >> from) & 1u) && (to / 5 == (b.white ? 5 : 0))) ? QUEEN : 0;
+  pos_out(pack(make_move(b, from, to, promo)), out);
+  return 0;
+}
+
+extern "C" int mtaz_pos_zeroing(const uint32_t pos[5], int code) {
+  const BB b = unpack(pos_in(pos));
+  int from, to;
+  if (host_decode(b, code, &from, &to)) return set_err(MTAZ_E_ILLEGAL, "action out of range");
+  return is_zeroing(b, from, to) ? 1 : 0;
+}
+
+extern "C" int mtaz_pos_encode(const uint32_t pos[5], uint8_t tokens[60], float* clock) {
+  const BB b = unpack(pos_in(pos));
+  encode_tokens(b, tokens);
+  *clock = encode_clock(b);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// numpy legacy RandomState (numpy/random/src/mt19937, src/legacy/legacy-distributions.c,
+// mtrand.pyx dirichlet / choice / randint).  One state per game.
+namespace {
+struct MTState {
+  uint32_t key[624];
+  int pos;
+  int has_gauss;
+  double gauss;
+};
+
+void mt_seed(MTState& s, uint32_t seed) {
+  for (int i = 0; i < 624; ++i) {
+    s.key[i] = seed;
+    seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(i + 1);
+  }
+  s.pos = 624;
+  s.has_gauss = 0;
+  s.gauss = 0.0;
+}
+
+void mt_gen(MTState& s) {
+  const uint32_t UPPER = 0x80000000u, LOWER = 0x7fffffffu, MATRIX_A = 0x9908b0dfu;
+  int i;
+  uint32_t y;
+  for (i = 0; i < 624 - 397; ++i) {
+    y = (s.key[i] & UPPER) | (s.key[i + 1] & LOWER);
+    s.key[i] = s.key[i + 397] ^ (y >> 1) ^ (-(y & 1u) & MATRIX_A);
+  }
+  for (; i < 623; ++i) {
+    y = (s.key[i] & UPPER) | (s.key[i + 1] & LOWER);
+    s.key[i] = s.key[i + (397 - 624)] ^ (y >> 1) ^ (-(y & 1u) & MATRIX_A);
+  }
+  y = (s.key[623] & UPPER) | (s.key[0] & LOWER);
+  s.key[623] = s.key[396] ^ (y >> 1) ^ (-(y & 1u) & MATRIX_A);
+  s.pos = 0;
+}
+
+inline uint32_t mt_next(MTState& s) {
+  if (s.pos == 624) mt_gen(s);
+  uint32_t y = s.key[s.pos++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+inline double legacy_double(MTState& s) {
+  const int32_t a = mt_next(s) >> 5;
+  const int32_t b = mt_next(s) >> 6;
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+double legacy_gauss(MTState& s) {
+  if (s.has_gauss) {
+    const double t = s.gauss;
+    s.has_gauss = 0;
+    s.gauss = 0.0;
+    return t;
+  }
+  double f, x1, x2, r2;
+  do {
+    x1 = 2.0 * legacy_double(s) - 1.0;
+    x2 = 2.0 * legacy_double(s) - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+  } while (r2 >= 1.0 || r2 == 0.0);
+  f = sqrt(-2.0 * log(r2) / r2);
+  s.gauss = f * x1;
+  s.has_gauss = 1;
+  return f * x2;
+}
+
+inline double legacy_exponential(MTState& s) { return -log(1.0 - legacy_double(s)); }
+
+double legacy_gamma(MTState& s, double shape) {
+  if (shape == 1.0) return legacy_exponential(s);
+  if (shape == 0.0) return 0.0;
+  if (shape < 1.0) {
+    for (;;) {
+      const double U = legacy_double(s);
+      const double V = legacy_exponential(s);
+      if (U <= 1.0 - shape) {
+        const double X = pow(U, 1. / shape);
+        if (X <= V) return X;
+      } else {
+        const double Y = -log((1 - U) / shape);
+        const double X = pow(1.0 - shape + shape * Y, 1. / shape);
+        if (X <= (V + Y)) return X;
+      }
+    }
+  }
+  const double b = shape - 1. / 3.;
+  const double c = 1. / sqrt(9 * b);
+  for (;;) {
+    double X, V;
+    do {
+      X = legacy_gauss(s);
+      V = 1.0 + c * X;
+    } while (V <= 0.0);
+    V = V * V * V;
+    const double U = legacy_double(s);
+    if (U < 1.0 - 0.0331 * (X * X) * (X * X)) return b * V;
+    if (log(U) < 0.5 * X * X + b * (1. - V + log(V))) return b * V;
+  }
+}
+
+void legacy_dirichlet(MTState& s, double alpha, int k, double* out) {
+  double acc = 0.0;
+  for (int j = 0; j < k; ++j) {
+    out[j] = legacy_gamma(s, alpha);
+    acc = acc + out[j];
+  }
+  const double invacc = 1 / acc;
+  for (int j = 0; j < k; ++j) out[j] = out[j] * invacc;
+}
+
+int64_t legacy_choice_p(MTState& s, const double* p, int k) {
+  // cdf = p.cumsum(); cdf /= cdf[-1]; searchsorted(random_sample(), side='right')
+  double cdf[KMAX];
+  double acc = 0.0;
+  for (int i = 0; i < k; ++i) { acc = acc + p[i]; cdf[i] = acc; }
+  const double last = cdf[k - 1];
+  for (int i = 0; i < k; ++i) cdf[i] = cdf[i] / last;
+  const double u = legacy_double(s);
+  int64_t idx = 0;
+  while (idx < k && cdf[idx] <= u) ++idx;
+  return idx;
+}
+
+int64_t legacy_randint(MTState& s, int64_t m) {
+  // randint(0, m): rng = m - 1, masked rejection on 32-bit draws; rng == 0 draws nothing
+  const uint64_t rng = (uint64_t)(m - 1);
+  if (rng == 0) return 0;
+  uint64_t mask = rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+  if (rng == 0xffffffffull) return mt_next(s);
+  uint32_t v;
+  while ((v = (mt_next(s) & (uint32_t)mask)) > rng) {
+  }
+  return v;
+}
+}  // namespace
+
+extern "C" size_t mtaz_rng_state_size(void) { return sizeof(MTState); }
+extern "C" void mtaz_rng_seed(void* st, uint32_t seed) { mt_seed(*(MTState*)st, seed); }
+extern "C" double mtaz_rng_double(void* st) { return legacy_double(*(MTState*)st); }
+extern "C" void mtaz_rng_dirichlet(void* st, double alpha, int k, double* out) { legacy_dirichlet(*(MTState*)st, alpha, k, out); }
+extern "C" int64_t mtaz_rng_choice_p(void* st, const double* p, int k) {
+  if (k <= 0 || k > KMAX) return set_err(MTAZ_E_CAPACITY, "choice size %d", k);
+  return legacy_choice_p(*(MTState*)st, p, k);
+}
+extern "C" int64_t mtaz_rng_randint(void* st, int64_t m) { return legacy_randint(*(MTState*)st, m); }
+
+// ---------------------------------------------------------------------------------------
+// batched rules kernels
+extern "C" int mtaz_legal_batch(int device, const uint32_t* d_pos, int n, uint32_t flags, int move_cap, uint16_t* d_codes,
+                                int32_t* d_counts, uint32_t* d_masks, int32_t* d_outcomes, void* stream) {
+  if (int e = ensure_codec_device(device)) return e;
+  launch_legal_batch(reinterpret_cast<const Pos*>(d_pos), n, flags, move_cap, d_codes, d_counts, d_masks, d_outcomes,
+                     (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int mtaz_encode_batch(int device, const uint32_t* d_pos, int n, uint8_t* d_tokens, float* d_clocks, void* stream) {
+  HIPCHK(hipSetDevice(device));
+  launch_encode_batch(reinterpret_cast<const Pos*>(d_pos), n, d_tokens, d_clocks, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// engine
+namespace {
+struct PlyRec {
+  Pos pos;
+  int32_t action;
+  std::vector<uint16_t> codes;
+  std::vector<uint32_t> visits;
+};
+
+enum Stat {
+  ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
+  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_COUNT
+};
+
+template <class F>
+void parallel_for(int n, F f) {
+  int nt = (int)std::thread::hardware_concurrency();
+  nt = std::max(1, std::min(nt, 16));
+  if (n < 64 || nt == 1) {
+    for (int i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int chunk = (n + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
+    const int a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    th.emplace_back([=, &f]() { for (int i = a; i < b; ++i) f(i); });
+  }
+  for (auto& x : th) x.join();
+}
+
+double now_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+}  // namespace
+
+struct mtaz_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int G = 0, sims = 0, tau = 6, cast_mode = 2, move_cap = 30;
+  double cpuct = 1.0, alpha = 0.6, eps = 0.25;
+  uint64_t seed_base = 0;
+  uint32_t flags = RF_DEFAULT;
+  Dev d{};
+  NetWeights w{};
+  NetBuffers nb{};
+  bool weights_ok = false;
+  std::vector<void*> allocs;
+  float* wbuf = nullptr;
+  // scratch
+  int32_t* d_actions = nullptr;
+  uint16_t* d_root_codes = nullptr;
+  uint32_t* d_root_visits = nullptr;
+  uint16_t* d_leaf_codes = nullptr;
+  int32_t* d_leaf_k = nullptr;
+  int32_t* d_trees = nullptr;
+  int32_t* d_count_log = nullptr;
+  double* d_sqrt = nullptr;
+  int count_log_cap = 0;
+  size_t noise_cap = 0;
+  std::vector<MTState> rng;
+  std::vector<std::vector<PlyRec>> rec;
+  std::vector<int32_t> final_outcome;
+  int n_played = 0;
+  double stats[ST_COUNT] = {0};
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  int wave = 0;
+
+  ~mtaz_engine() {
+    if (device >= 0) (void)hipSetDevice(device);
+    for (auto e : ev) (void)hipEventDestroy(e);
+    for (void* p : allocs) (void)hipFree(p);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  template <class T>
+  int dalloc(T** p, size_t n) {
+    void* q = nullptr;
+    const size_t bytes = std::max<size_t>(n * sizeof(T), 16);
+    HIPCHK(hipMalloc(&q, bytes));
+    allocs.push_back(q);
+    *p = (T*)q;
+    return 0;
+  }
+};
+
+#define ECHK(x)            \
+  do {                     \
+    int e_ = (x);          \
+    if (e_ < 0) return e_; \
+  } while (0)
+
+static int engine_alloc(mtaz_engine* h) {
+  const int G = h->G, T = 2 * G;
+  Trees& tr = h->d.tr;
+  Games& gm = h->d.gm;
+  Leaves& lf = h->d.lf;
+  const int max_moves = h->move_cap > 0 ? h->move_cap : 200;     // searches per agent per game
+  tr.NC = h->sims * max_moves + 2;
+  int hc = 1;
+  while (hc < 2 * tr.NC) hc <<= 1;
+  tr.HC = hc;
+  tr.EC = tr.NC * 16;
+  gm.DMAX = 2 * max_moves + 8;
+  gm.HMAX = 2 * max_moves + 8;
+  const size_t TN = (size_t)T * tr.NC, TE = (size_t)T * tr.EC;
+  ECHK(h->dalloc(&tr.node_pos, TN));
+  ECHK(h->dalloc(&tr.node_e0, TN));
+  ECHK(h->dalloc(&tr.node_k, TN));
+  ECHK(h->dalloc(&tr.node_term, TN));
+  ECHK(h->dalloc(&tr.node_tval, TN));
+  ECHK(h->dalloc(&tr.node_sumN, TN));
+  ECHK(h->dalloc(&tr.hash, (size_t)T * tr.HC));
+  ECHK(h->dalloc(&tr.n_nodes, T));
+  ECHK(h->dalloc(&tr.n_edges, T));
+  ECHK(h->dalloc(&tr.e_code, TE));
+  ECHK(h->dalloc(&tr.e_P, TE));
+  ECHK(h->dalloc(&tr.e_Q, TE));
+  ECHK(h->dalloc(&tr.e_N, TE));
+  HIPCHK(hipMemset(tr.hash, 0, (size_t)T * tr.HC * 4));
+  HIPCHK(hipMemset(tr.n_nodes, 0, T * 4));
+  HIPCHK(hipMemset(tr.n_edges, 0, T * 4));
+  ECHK(h->dalloc(&gm.root, G));
+  ECHK(h->dalloc(&gm.agent, G));
+  ECHK(h->dalloc(&gm.active, G));
+  ECHK(h->dalloc(&gm.outcome, G));
+  ECHK(h->dalloc(&gm.root_new, G));
+  ECHK(h->dalloc(&gm.root_k, G));
+  ECHK(h->dalloc(&gm.noise_off, G));
+  ECHK(h->dalloc(&gm.path_node, (size_t)G * gm.DMAX));
+  ECHK(h->dalloc(&gm.path_edge, (size_t)G * gm.DMAX));
+  ECHK(h->dalloc(&gm.path_len, G));
+  ECHK(h->dalloc(&gm.hist, (size_t)G * gm.HMAX));
+  ECHK(h->dalloc(&gm.nhist, G));
+  HIPCHK(hipMemset(gm.active, 0, G));
+  HIPCHK(hipMemset(gm.agent, 0, G * 4));
+  HIPCHK(hipMemset(gm.nhist, 0, G * 4));
+  HIPCHK(hipMemset(gm.outcome, 0, G * 4));
+  h->noise_cap = (size_t)G * h->sims * 16;
+  ECHK(h->dalloc(&gm.noise, h->noise_cap));
+  ECHK(h->dalloc(&lf.count, 1));
+  ECHK(h->dalloc(&lf.game, G));
+  ECHK(h->dalloc(&lf.tree, G));
+  ECHK(h->dalloc(&lf.node, G));
+  ECHK(h->dalloc(&lf.pos, G));
+  ECHK(h->dalloc(&lf.P, (size_t)G * KMAX));
+  ECHK(h->dalloc(&lf.v, G));
+  ECHK(h->dalloc(&h->d_actions, G));
+  ECHK(h->dalloc(&h->d_root_codes, (size_t)G * KMAX));
+  ECHK(h->dalloc(&h->d_root_visits, (size_t)G * KMAX));
+  ECHK(h->dalloc(&h->d_leaf_codes, (size_t)G * KMAX));
+  ECHK(h->dalloc(&h->d_leaf_k, G));
+  ECHK(h->dalloc(&h->d_trees, T));
+  h->count_log_cap = h->sims * (2 * max_moves + 8);
+  ECHK(h->dalloc(&h->d_count_log, h->count_log_cap));
+  // exact sqrt(N.sum()) table: N.sum() <= sims * searches per agent
+  const int sqn = tr.NC + 2;
+  std::vector<double> sq(sqn);
+  for (int i = 0; i < sqn; ++i) sq[i] = sqrt((double)i);
+  ECHK(h->dalloc(&h->d_sqrt, sqn));
+  HIPCHK(hipMemcpy(h->d_sqrt, sq.data(), sqn * 8, hipMemcpyHostToDevice));
+  ECHK(h->dalloc(&h->d.pr.err, 1));
+  HIPCHK(hipMemset(h->d.pr.err, 0, 4));
+  Params& pr = h->d.pr;
+  pr.G = G;
+  pr.sims = h->sims;
+  pr.cpuct = h->cpuct;
+  pr.cpuct_f = (float)h->cpuct;
+  pr.cast_mode = h->cast_mode;
+  pr.flags = h->flags;
+  pr.move_cap = h->move_cap;
+  pr.sqrt_tab = h->d_sqrt;
+  pr.sqrt_n = sqn;
+  // network activations: [G][256][32] x 3
+  h->nb.B = G;
+  ECHK(h->dalloc(&h->nb.x0, (size_t)G * 8192));
+  ECHK(h->dalloc(&h->nb.x1, (size_t)G * 8192));
+  ECHK(h->dalloc(&h->nb.t, (size_t)G * 8192));
+  h->rng.resize(G);
+  return 0;
+}
+
+extern "C" mtaz_engine* mtaz_create(int device, int n_games, int sims, double cpuct, int tau_change, double dir_alpha,
+                                    double dir_eps, uint64_t seed_base, int numpy_cast_mode, uint32_t rules_flags,
+                                    int move_cap) {
+  if (n_games <= 0 || sims <= 0) { set_err(MTAZ_E_FAIL, "n_games and sims must be positive"); return nullptr; }
+  if (numpy_cast_mode != 1 && numpy_cast_mode != 2) { set_err(MTAZ_E_FAIL, "numpy_cast_mode must be 1 or 2"); return nullptr; }
+  // the PUCT kernel hard-codes the reference's 0.75 / 0.25 mix (exp/agent.py:82)
+  if (dir_eps != 0.25 || !(dir_alpha > 0)) {
+    set_err(MTAZ_E_FAIL, "dir_eps must be 0.25 (exp/agent.py:82) and dir_alpha > 0");
+    return nullptr;
+  }
+  if (ensure_codec_device(device)) return nullptr;
+  mtaz_engine* h = new mtaz_engine();
+  h->device = device;
+  h->G = n_games;
+  h->sims = sims;
+  h->cpuct = cpuct;
+  h->tau = tau_change;
+  h->alpha = dir_alpha;
+  h->eps = dir_eps;
+  h->seed_base = seed_base;
+  h->cast_mode = numpy_cast_mode;
+  h->flags = rules_flags;
+  h->move_cap = move_cap;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess || engine_alloc(h) < 0) {
+    const std::string e = g_err.empty() ? "engine allocation failed" : g_err;
+    delete h;
+    set_err(MTAZ_E_DEVICE, "%s", e.c_str());
+    return nullptr;
+  }
+  return h;
+}
+
+extern "C" void mtaz_destroy(mtaz_engine* h) { delete h; }
+
+static int check_err(mtaz_engine* h) {
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, h->d.pr.err, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (e) {
+    HIPCHK(hipMemsetAsync(h->d.pr.err, 0, 4, h->stream));
+    std::string m;
+    if (e & ERR_NODES) m += " node-capacity";
+    if (e & ERR_EDGES) m += " edge-capacity";
+    if (e & ERR_DEPTH) m += " search-depth";
+    if (e & ERR_KMAX) m += " legal-list>256";
+    if (e & ERR_SQRT) m += " visit-sum";
+    if (e & ERR_ROOT) m += " root-state";
+    if (e & ERR_ILLEGAL) m += " illegal-action";
+    if (e & ERR_HIST) m += " history-capacity";
+    if (e & ERR_HASH) m += " hash-full";
+    return set_err((e & ERR_ILLEGAL) ? MTAZ_E_ILLEGAL : MTAZ_E_CAPACITY, "device error flags 0x%x:%s", e, m.c_str());
+  }
+  return 0;
+}
+
+// ---- weights --------------------------------------------------------------------------
+extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, const int64_t* numels, int n) {
+  if (n != 133) return set_err(MTAZ_E_FAIL, "expected 133 state_dict tensors (num_batches_tracked skipped), got %d", n);
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<std::vector<float>> t(n);
+  for (int i = 0; i < n; ++i) {
+    t[i].resize(numels[i]);
+    HIPCHK(hipMemcpy(t[i].data(), d_tensors[i], numels[i] * 4, hipMemcpyDeviceToHost));
+  }
+  auto expect = [&](int i, int64_t ne) { return numels[i] == ne; };
+  // layout checks (exp/policy.py:54-69)
+  bool ok = expect(0, 28) && expect(1, 256 * 8 * 9) && expect(121, 554 * 61) && expect(122, 554) && expect(123, 256) &&
+            expect(129, 256 * 31) && expect(130, 256) && expect(131, 256) && expect(132, 1) && expect(115, 512);
+  for (int j = 0; j < 18 && ok; ++j) ok = expect(7 + j * 6, 256 * 256 * 9) && expect(8 + j * 6, 256);
+  if (!ok) return set_err(MTAZ_E_FAIL, "state_dict tensor sizes do not match exp/policy.py Network");
+  const double bn_eps = 1e-5;   // torch.nn.BatchNorm2d default (exp/policy.py:32)
+  // conv at tensor index base: w, b, gamma, beta, mean, var -> folded scale/shift per out channel
+  auto fold = [&](int base, int cout, std::vector<double>& scale, std::vector<double>& shift) {
+    scale.resize(cout);
+    shift.resize(cout);
+    for (int c = 0; c < cout; ++c) {
+      const double s = (double)t[base + 2][c] / sqrt((double)t[base + 5][c] + bn_eps);
+      scale[c] = s;
+      shift[c] = ((double)t[base + 1][c] - (double)t[base + 4][c]) * s + (double)t[base + 3][c];
+    }
+  };
+  const size_t n_emb = 28, n_stem = 256 * 72 + 256, n_conv = (size_t)CONV_LAYERS * (CONV_W_FLOATS + 256);
+  const size_t n_heads = 512 + 2 + 554 * 61 + 554 + 256 + 1 + 256 * 31 + 256 + 256 + 1;
+  const size_t total = n_emb + n_stem + n_conv + n_heads + 64;
+  std::vector<float> buf(total, 0.f);
+  size_t off = 0;
+  auto take = [&](size_t cnt) { size_t o = off; off += (cnt + 15) & ~(size_t)15; return o; };
+  const size_t o_emb = take(28), o_stem_w = take(256 * 72), o_stem_b = take(256);
+  const size_t o_conv_w = take((size_t)CONV_LAYERS * CONV_W_FLOATS), o_conv_b = take(CONV_LAYERS * 256);
+  const size_t o_pw = take(512), o_pb = take(2), o_plw = take(554 * 61), o_plb = take(554), o_vw = take(256),
+               o_vb = take(1), o_v1w = take(256 * 31), o_v1b = take(256), o_v2w = take(256), o_v2b = take(1);
+  if (off > buf.size()) buf.resize(off);
+  std::copy(t[0].begin(), t[0].end(), buf.begin() + o_emb);
+  std::vector<double> sc, sh;
+  fold(1, 256, sc, sh);
+  for (int co = 0; co < 256; ++co) {
+    for (int j = 0; j < 72; ++j) buf[o_stem_w + co * 72 + j] = (float)(t[1][co * 72 + j] * sc[co]);
+    buf[o_stem_b + co] = (float)sh[co];
+  }
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const int base = 7 + L * 6;
+    fold(base, 256, sc, sh);
+    const std::vector<float>& W = t[base];   // [co][ci][3][3]
+    float* dst = buf.data() + o_conv_w + (size_t)L * CONV_W_FLOATS;
+    for (int ct = 0; ct < 8; ++ct)
+      for (int q = 0; q < 288; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 4; ++e) {
+            const int s = 4 * q + e, k = 2 * s + (lane >> 5);
+            const int tap = k >> 8, ci = k & 255, co = ct * 32 + (lane & 31);
+            dst[(((size_t)ct * 288 + q) * 64 + lane) * 4 + e] = (float)(W[((size_t)co * 256 + ci) * 9 + tap] * sc[co]);
+          }
+    for (int co = 0; co < 256; ++co) buf[o_conv_b + L * 256 + co] = (float)sh[co];
+  }
+  fold(115, 2, sc, sh);
+  for (int o = 0; o < 2; ++o) {
+    for (int c = 0; c < 256; ++c) buf[o_pw + o * 256 + c] = (float)(t[115][o * 256 + c] * sc[o]);
+    buf[o_pb + o] = (float)sh[o];
+  }
+  std::copy(t[121].begin(), t[121].end(), buf.begin() + o_plw);
+  std::copy(t[122].begin(), t[122].end(), buf.begin() + o_plb);
+  fold(123, 1, sc, sh);
+  for (int c = 0; c < 256; ++c) buf[o_vw + c] = (float)(t[123][c] * sc[0]);
+  buf[o_vb] = (float)sh[0];
+  std::copy(t[129].begin(), t[129].end(), buf.begin() + o_v1w);
+  std::copy(t[130].begin(), t[130].end(), buf.begin() + o_v1b);
+  std::copy(t[131].begin(), t[131].end(), buf.begin() + o_v2w);
+  buf[o_v2b] = t[132][0];
+  if (!h->wbuf) ECHK(h->dalloc(&h->wbuf, buf.size()));
+  HIPCHK(hipMemcpy(h->wbuf, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+  float* b = h->wbuf;
+  h->w.emb = b + o_emb;
+  h->w.stem_w = b + o_stem_w;
+  h->w.stem_b = b + o_stem_b;
+  h->w.conv_w = b + o_conv_w;
+  h->w.conv_b = b + o_conv_b;
+  h->w.pconv_w = b + o_pw;
+  h->w.pconv_b = b + o_pb;
+  h->w.plin_w = b + o_plw;
+  h->w.plin_b = b + o_plb;
+  h->w.vconv_w = b + o_vw;
+  h->w.vconv_b = b + o_vb;
+  h->w.vl1_w = b + o_v1w;
+  h->w.vl1_b = b + o_v1b;
+  h->w.vl2_w = b + o_v2w;
+  h->w.vl2_b = b + o_v2b;
+  h->weights_ok = true;
+  return 0;
+}
+
+extern "C" int mtaz_evaluate(mtaz_engine* h, const uint32_t* d_pos, int n, float* d_logits, float* d_values) {
+  if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
+  HIPCHK(hipSetDevice(h->device));
+  for (int s = 0; s < n; s += h->G) {
+    const int m = std::min(h->G, n - s);
+    NetBuffers nb = h->nb;
+    nb.logits = d_logits + (size_t)s * NUM_ACTIONS;
+    launch_net(h->d, h->w, nb, reinterpret_cast<const Pos*>(d_pos) + s, nullptr, m, NET_FULL_LOGITS, d_values + s,
+               h->stream, nullptr, nullptr);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// ---- fine-grained search API ----------------------------------------------------------------
+extern "C" int mtaz_set_games(mtaz_engine* h, const uint32_t* roots, const int32_t* agents, const uint8_t* active, int n) {
+  if (n > h->G) return set_err(MTAZ_E_CAPACITY, "n=%d > engine games %d", n, h->G);
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<uint8_t> act(h->G, 0);
+  std::vector<int32_t> ag(h->G, 0), zero(h->G, 0);
+  std::vector<Pos> rt(h->G);
+  for (int g = 0; g < n; ++g) {
+    act[g] = active ? active[g] : 1;
+    ag[g] = agents ? agents[g] : 0;
+    rt[g] = pos_in(roots + 5 * g);
+  }
+  HIPCHK(hipMemcpyAsync(h->d.gm.root, rt.data(), h->G * sizeof(Pos), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.gm.agent, ag.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.gm.active, act.data(), h->G, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.gm.nhist, zero.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.gm.outcome, zero.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int mtaz_get_games(mtaz_engine* h, uint32_t* roots, int32_t* agents, uint8_t* active, int32_t* outcome) {
+  HIPCHK(hipSetDevice(h->device));
+  if (roots) HIPCHK(hipMemcpyAsync(roots, h->d.gm.root, h->G * sizeof(Pos), hipMemcpyDeviceToHost, h->stream));
+  if (agents) HIPCHK(hipMemcpyAsync(agents, h->d.gm.agent, h->G * 4, hipMemcpyDeviceToHost, h->stream));
+  if (active) HIPCHK(hipMemcpyAsync(active, h->d.gm.active, h->G, hipMemcpyDeviceToHost, h->stream));
+  if (outcome) HIPCHK(hipMemcpyAsync(outcome, h->d.gm.outcome, h->G * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n) {
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<int32_t> all;
+  if (!trees) {
+    all.resize(2 * h->G);
+    for (int i = 0; i < 2 * h->G; ++i) all[i] = i;
+    trees = all.data();
+    n = 2 * h->G;
+  }
+  if (n > 2 * h->G) return set_err(MTAZ_E_CAPACITY, "too many trees");
+  for (int i = 0; i < n; ++i)
+    if (trees[i] < 0 || trees[i] >= 2 * h->G) return set_err(MTAZ_E_FAIL, "tree index %d out of range", trees[i]);
+  HIPCHK(hipMemcpyAsync(h->d_trees, trees, n * 4, hipMemcpyHostToDevice, h->stream));
+  launch_reset_trees(h->d, h->d_trees, n, h->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int mtaz_move_begin(mtaz_engine* h, int32_t* root_k, int32_t* root_new) {
+  HIPCHK(hipSetDevice(h->device));
+  launch_move_begin(h->d, h->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(root_k, h->d.gm.root_k, h->G * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(root_new, h->d.gm.root_new, h->G * 4, hipMemcpyDeviceToHost, h->stream));
+  return check_err(h);
+}
+
+extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, int64_t total) {
+  HIPCHK(hipSetDevice(h->device));
+  if ((size_t)total > h->noise_cap) {
+    // grow (rare: long legal lists)
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, total * 8));
+    h->allocs.push_back(q);
+    h->d.gm.noise = (double*)q;
+    h->noise_cap = total;
+  }
+  if (total > 0) HIPCHK(hipMemcpyAsync(h->d.gm.noise, noise, total * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offsets, h->G * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+static int sim_gpu(mtaz_engine* h, int sim) {
+  HIPCHK(hipMemsetAsync(h->d.lf.count, 0, 4, h->stream));
+  launch_select(h->d, sim, h->stream);
+  hipEvent_t eb = nullptr, ee = nullptr;
+  if (h->timing) {
+    const size_t need = 2 * (size_t)(h->wave + 1);
+    while (h->ev.size() < need) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      h->ev.push_back(e);
+    }
+    eb = h->ev[2 * h->wave];
+    ee = h->ev[2 * h->wave + 1];
+  }
+  launch_net(h->d, h->w, h->nb, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, h->stream, eb, ee);
+  launch_backup(h->d, h->stream);
+  if (h->wave < h->count_log_cap)
+    HIPCHK(hipMemcpyAsync(h->d_count_log + h->wave, h->d.lf.count, 4, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(hipGetLastError());
+  ++h->wave;
+  return 0;
+}
+
+extern "C" int mtaz_simulate(mtaz_engine* h, int first_sim, int n_sims) {
+  if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
+  HIPCHK(hipSetDevice(h->device));
+  for (int s = first_sim; s < first_sim + n_sims; ++s) ECHK(sim_gpu(h, s));
+  return check_err(h);
+}
+
+extern "C" int mtaz_sim_select(mtaz_engine* h, int sim) {
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemsetAsync(h->d.lf.count, 0, 4, h->stream));
+  launch_select(h->d, sim, h->stream);
+  HIPCHK(hipGetLastError());
+  return check_err(h);
+}
+
+extern "C" int mtaz_leaves_get(mtaz_engine* h, int32_t* count, uint32_t* pos, int32_t* game, int32_t* k, uint16_t* codes) {
+  HIPCHK(hipSetDevice(h->device));
+  int32_t c = 0;
+  HIPCHK(hipMemcpyAsync(&c, h->d.lf.count, 4, hipMemcpyDeviceToHost, h->stream));
+  launch_gather_leaf_codes(h->d, h->d_leaf_codes, h->d_leaf_k, h->stream);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *count = c;
+  if (c > 0) {
+    HIPCHK(hipMemcpyAsync(pos, h->d.lf.pos, c * sizeof(Pos), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(game, h->d.lf.game, c * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(k, h->d_leaf_k, c * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(codes, h->d_leaf_codes, (size_t)c * KMAX * 2, hipMemcpyDeviceToHost, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int mtaz_leaves_set(mtaz_engine* h, const float* P, const float* v, int count) {
+  HIPCHK(hipSetDevice(h->device));
+  if (count > 0) {
+    HIPCHK(hipMemcpyAsync(h->d.lf.P, P, (size_t)count * KMAX * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d.lf.v, v, count * 4, hipMemcpyHostToDevice, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+extern "C" int mtaz_sim_backup(mtaz_engine* h) {
+  HIPCHK(hipSetDevice(h->device));
+  launch_backup(h->d, h->stream);
+  HIPCHK(hipGetLastError());
+  return check_err(h);
+}
+
+extern "C" int mtaz_move_end(mtaz_engine* h, uint16_t* codes, uint32_t* visits, int32_t* k, int kout) {
+  HIPCHK(hipSetDevice(h->device));
+  if (kout > KMAX) kout = KMAX;
+  launch_move_end(h->d, h->d_root_codes, h->d_root_visits, kout, h->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(codes, h->d_root_codes, (size_t)h->G * kout * 2, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(visits, h->d_root_visits, (size_t)h->G * kout * 4, hipMemcpyDeviceToHost, h->stream));
+  if (k) HIPCHK(hipMemcpyAsync(k, h->d.gm.root_k, h->G * 4, hipMemcpyDeviceToHost, h->stream));
+  return check_err(h);
+}
+
+extern "C" int mtaz_apply(mtaz_engine* h, const int32_t* actions) {
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(h->d_actions, actions, h->G * 4, hipMemcpyHostToDevice, h->stream));
+  launch_apply(h->d, h->d_actions, h->stream);
+  HIPCHK(hipGetLastError());
+  return check_err(h);
+}
+
+extern "C" int mtaz_tree_size(mtaz_engine* h, int tree, int32_t* nodes, int32_t* edges) {
+  if (tree < 0 || tree >= 2 * h->G) return set_err(MTAZ_E_FAIL, "tree out of range");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpy(nodes, h->d.tr.n_nodes + tree, 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(edges, h->d.tr.n_edges + tree, 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int mtaz_tree_get(mtaz_engine* h, int tree, uint32_t* pos, uint32_t* e0, uint16_t* k, uint8_t* term,
+                             double* tval, uint16_t* codes, float* P, double* Q, uint32_t* N) {
+  int32_t nn = 0, ne = 0;
+  ECHK(mtaz_tree_size(h, tree, &nn, &ne));
+  const Trees& T = h->d.tr;
+  const size_t nb = (size_t)tree * T.NC, eb = (size_t)tree * T.EC;
+  HIPCHK(hipMemcpy(pos, T.node_pos + nb, nn * sizeof(Pos), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(e0, T.node_e0 + nb, nn * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(k, T.node_k + nb, nn * 2, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(term, T.node_term + nb, nn, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(tval, T.node_tval + nb, nn * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(codes, T.e_code + eb, ne * 2, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(P, T.e_P + eb, ne * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Q, T.e_Q + eb, ne * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(N, T.e_N + eb, ne * 4, hipMemcpyDeviceToHost));
+  return nn;
+}
+
+extern "C" int mtaz_set_timing(mtaz_engine* h, int on) {
+  h->timing = on != 0;
+  return 0;
+}
+
+// ---- batched self-play ------------------------------------------------------------------------
+// Per move: move_begin -> host draws each game's Dirichlet vectors (numpy legacy, exact)
+// -> `sims` GPU waves of select / network / backup with no host sync -> root visit
+// counts -> host action choice (choice with p while fullmove < tau, else argmax with a
+// random tie-break, exp/agent.py:110-119) -> apply on device.
+extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
+  if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
+  if (n_games > h->G || n_games <= 0) return set_err(MTAZ_E_CAPACITY, "n_games=%d (engine has %d)", n_games, h->G);
+  HIPCHK(hipSetDevice(h->device));
+  const double t0 = now_ms();
+  const int G = h->G;
+  for (int i = 0; i < ST_COUNT; ++i) h->stats[i] = 0;
+  if (!from_current) {
+    uint32_t start[5];
+    ECHK(mtaz_pos_from_fen("2nbk/2ppp/5/5/PPP2/KBN2 w 0 1", start));   // exp/environment.py:6
+    std::vector<uint32_t> roots((size_t)G * 5);
+    std::vector<uint8_t> act(G, 0);
+    for (int g = 0; g < G; ++g) {
+      memcpy(&roots[5 * g], start, 20);
+      act[g] = g < n_games;
+    }
+    ECHK(mtaz_set_games(h, roots.data(), nullptr, act.data(), G));
+  }
+  ECHK(mtaz_clear_trees(h, nullptr, 0));
+  for (int g = 0; g < G; ++g) mt_seed(h->rng[g], (uint32_t)(h->seed_base + (uint64_t)g));
+  h->rec.assign(G, {});
+  h->final_outcome.assign(G, 0);
+  h->wave = 0;
+  h->n_played = n_games;
+
+  std::vector<uint8_t> active(G);
+  std::vector<int32_t> agents(G), outcome_v(G), root_k(G), root_new(G), actions(G, 0);
+  std::vector<uint32_t> roots((size_t)G * 5);
+  std::vector<int64_t> offs(G);
+  std::vector<double> noise;
+  std::vector<uint16_t> codes((size_t)G * KMAX);
+  std::vector<uint32_t> visits((size_t)G * KMAX);
+  ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
+  double rng_ms = 0, sync_ms = 0;
+  int moves = 0;
+  for (;;) {
+    int n_active = 0;
+    for (int g = 0; g < G; ++g) n_active += active[g];
+    if (!n_active) break;
+    double ts = now_ms();
+    ECHK(mtaz_move_begin(h, root_k.data(), root_new.data()));
+    sync_ms += now_ms() - ts;
+    // Dirichlet draws: sims - root_new vectors of size k per active game
+    double tr = now_ms();
+    int64_t total = 0;
+    for (int g = 0; g < G; ++g) {
+      offs[g] = total;
+      if (active[g]) total += (int64_t)(h->sims - root_new[g]) * root_k[g];
+    }
+    noise.resize(std::max<int64_t>(total, 1));
+    parallel_for(G, [&](int g) {
+      if (!active[g]) return;
+      const int k = root_k[g];
+      double* out = noise.data() + offs[g];
+      for (int j = 0; j < h->sims - root_new[g]; ++j) legacy_dirichlet(h->rng[g], h->alpha, k, out + (size_t)j * k);
+    });
+    rng_ms += now_ms() - tr;
+    ECHK(mtaz_set_noise(h, noise.data(), offs.data(), total));
+    for (int s = 0; s < h->sims; ++s) ECHK(sim_gpu(h, s));
+    ts = now_ms();
+    ECHK(mtaz_move_end(h, codes.data(), visits.data(), nullptr, KMAX));
+    sync_ms += now_ms() - ts;
+    // action selection (exp/agent.py:110-119) + records (exp/callbacks.py:40-47)
+    tr = now_ms();
+    parallel_for(G, [&](int g) {
+      if (!active[g]) return;
+      const int k = root_k[g];
+      const uint16_t* c = codes.data() + (size_t)g * KMAX;
+      const uint32_t* v = visits.data() + (size_t)g * KMAX;
+      double pi[KMAX];
+      double sum = 0;
+      for (int i = 0; i < k; ++i) sum += (double)v[i];
+      for (int i = 0; i < k; ++i) pi[i] = (double)v[i] / sum;
+      const int fullmove = (int)(roots[5 * g + 4] >> 16);
+      int idx;
+      if (fullmove < h->tau) {
+        idx = (int)legacy_choice_p(h->rng[g], pi, k);
+      } else {
+        double mx = pi[0];
+        for (int i = 1; i < k; ++i) mx = std::max(mx, pi[i]);
+        int maxima[KMAX], m = 0;
+        for (int i = 0; i < k; ++i)
+          if (pi[i] == mx) maxima[m++] = i;
+        idx = maxima[legacy_randint(h->rng[g], m)];
+      }
+      actions[g] = c[idx];
+      PlyRec r;
+      r.pos = pos_in(&roots[5 * g]);
+      r.action = c[idx];
+      r.codes.assign(c, c + k);
+      r.visits.assign(v, v + k);
+      h->rec[g].push_back(std::move(r));
+    });
+    rng_ms += now_ms() - tr;
+    ts = now_ms();
+    ECHK(mtaz_apply(h, actions.data()));
+    ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
+    sync_ms += now_ms() - ts;
+    h->stats[ST_SIMS] += (double)n_active * h->sims;
+    ++moves;
+  }
+  for (int g = 0; g < G; ++g) h->final_outcome[g] = outcome_v[g];
+  // stats
+  std::vector<int32_t> counts(std::min(h->wave, h->count_log_cap));
+  if (!counts.empty())
+    HIPCHK(hipMemcpy(counts.data(), h->d_count_log, counts.size() * 4, hipMemcpyDeviceToHost));
+  double evals = 0;
+  for (int c : counts) evals += c;
+  double trunk_ms = 0, trunk_boards = 0;
+  if (h->timing) {
+    for (int wv = 0; wv < h->wave && wv < (int)counts.size(); ++wv) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, h->ev[2 * wv], h->ev[2 * wv + 1]));
+      trunk_ms += ms;
+      trunk_boards += counts[wv];
+    }
+  }
+  int64_t plies = 0, decisive = 0;
+  for (int g = 0; g < n_games; ++g) {
+    plies += (int64_t)h->rec[g].size();
+    decisive += h->final_outcome[g] == DECISIVE;
+  }
+  int32_t mxn = 0;
+  for (int t = 0; t < 2 * n_games && t < 64; ++t) {
+    int32_t nn, ne;
+    if (mtaz_tree_size(h, t, &nn, &ne) == 0) mxn = std::max(mxn, nn);
+  }
+  h->stats[ST_PLIES] = (double)plies;
+  h->stats[ST_NN_EVALS] = evals;
+  h->stats[ST_TERMINAL_SIMS] = h->stats[ST_SIMS] - evals;
+  h->stats[ST_TRUNK_MS] = trunk_ms;
+  h->stats[ST_TRUNK_BOARDS] = trunk_boards;
+  h->stats[ST_WAVES] = h->wave;
+  h->stats[ST_HOST_RNG_MS] = rng_ms;
+  h->stats[ST_WALL_MS] = now_ms() - t0;
+  h->stats[ST_GAMES] = n_games;
+  h->stats[ST_DECISIVE] = (double)decisive;
+  h->stats[ST_MOVES] = moves;
+  h->stats[ST_TRUNK_LAUNCHES] = h->timing ? 18.0 * h->wave : 0;
+  h->stats[ST_MAX_NODES] = mxn;
+  h->stats[ST_SYNC_MS] = sync_ms;
+  return 0;
+}
+
+extern "C" int mtaz_stats(mtaz_engine* h, double* out, int n) {
+  for (int i = 0; i < n && i < ST_COUNT; ++i) out[i] = h->stats[i];
+  return ST_COUNT;
+}
+
+extern "C" int mtaz_records_counts(mtaz_engine* h, int32_t* plies_per_game, int64_t* total_plies, int64_t* total_entries) {
+  int64_t tp = 0, te = 0;
+  for (int g = 0; g < h->n_played; ++g) {
+    plies_per_game[g] = (int32_t)h->rec[g].size();
+    tp += (int64_t)h->rec[g].size();
+    for (auto& r : h->rec[g]) te += (int64_t)r.codes.size();
+  }
+  *total_plies = tp;
+  *total_entries = te;
+  return 0;
+}
+
+// reward back-fill as exp/callbacks.py:49-54: last step's reward (1.0 decisive, 0.0 draw),
+// alternating sign towards the first step.
+extern "C" int mtaz_records_get(mtaz_engine* h, uint32_t* pos, int32_t* action, int32_t* k, uint16_t* codes,
+                                uint32_t* visits, float* reward, int32_t* outcome_out) {
+  int64_t p = 0, e = 0;
+  for (int g = 0; g < h->n_played; ++g) {
+    const auto& R = h->rec[g];
+    const int oc = h->final_outcome[g];
+    if (outcome_out) outcome_out[g] = oc;
+    float rw = oc == DECISIVE ? 1.0f : 0.0f;
+    std::vector<float> rws(R.size());
+    for (int i = (int)R.size() - 1; i >= 0; --i) {
+      rws[i] = rw;
+      rw = -rw;
+    }
+    for (size_t i = 0; i < R.size(); ++i, ++p) {
+      pos_out(R[i].pos, pos + 5 * p);
+      action[p] = R[i].action;
+      k[p] = (int32_t)R[i].codes.size();
+      reward[p] = rws[i];
+      memcpy(codes + e, R[i].codes.data(), R[i].codes.size() * 2);
+      memcpy(visits + e, R[i].visits.data(), R[i].visits.size() * 4);
+      e += (int64_t)R[i].codes.size();
+    }
+  }
+  return 0;
+}

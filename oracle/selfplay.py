@@ -108,6 +108,9 @@ def play_games(evaluator, num_games, sims, seed_base=0, cpuct=1, tau_change=6, c
         def on_episode_end(self):
             evals[0] += agents[0].mcts.nn_evals + agents[1].mcts.nn_evals
             terms[0] += agents[0].mcts.terminal_hits + agents[1].mcts.terminal_hits
+            if stats is not None:
+                # agent i's table; agent 0 moved first because the referee is reset per game
+                stats.setdefault('trees', []).append((agents[0].mcts._data, agents[1].mcts._data))
 
     run_episodes(env, referee, num_games, callbacks + [_Count()], on_episode_start=start)
     if stats is not None:

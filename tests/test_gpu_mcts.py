@@ -1,0 +1,134 @@
+"""GPU: MCTS kernels vs the CPU oracle / the reference's own traces, bit-exact.
+
+Parity tiers:
+  L1  tree + moves bit-exact with a host evaluator (the oracle's SyntheticEvaluator,
+      or the batch-1 torch-CPU seed-0 net exactly as the reference evaluates leaves)
+  L3  GPU network end to end: move identity rate vs the reference trace, reported
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from helpers import compare_records, drive_engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(n_games, sims, **kw):
+    from minitchess_alphazero_amd.engine import Engine
+    return Engine(n_games=n_games, sims=sims, **kw)
+
+
+def test_select_expand_backup_synthetic_vs_reference_traces():
+    """Host evaluator = SyntheticEvaluator: every game of the reference trace fixture."""
+    from oracle.mcts import SyntheticEvaluator
+    t = load_golden('trees')
+    ev = SyntheticEvaluator(salt=t['synthetic_salt'])
+    by_sims = {}
+    for gm in t['synthetic']:
+        by_sims.setdefault(gm['sims'], []).append(gm)
+    for sims, games in by_sims.items():
+        eng = _engine(len(games), sims)
+        recs, _ = drive_engine(eng, len(games), sims, [g['seed'] for g in games], evaluator=ev)
+        for got, gm in zip(recs, games):
+            same, total, first = compare_records(got, gm['moves'])
+            assert first is None, f'seed {gm["seed"]} sims {sims}: first mismatch at ply {first}'
+            assert [r['reward'] for r in got] == [r['reward'] for r in gm['moves']]
+
+
+def test_trees_bit_exact_vs_oracle():
+    """Final transposition tables (Q, N, P, legal_moves, terminal, visited) equal the oracle's."""
+    from oracle.mcts import SyntheticEvaluator
+    from oracle import selfplay
+    ev = SyntheticEvaluator(salt=3)
+    seeds = [101, 102, 103]
+    eng = _engine(len(seeds), 24)
+    trees = []
+    recs, _ = drive_engine(eng, len(seeds), 24, seeds, evaluator=ev, trees_out=trees)
+    for g, s in enumerate(seeds):
+        st = {}
+        ref = selfplay.play_games(ev, 1, 24, seed_base=s, stats=st)[0]
+        assert compare_records(recs[g], ref)[2] is None
+        for agent in (0, 1):
+            mine, theirs = trees[g][agent], st['trees'][0][agent]
+            assert mine['visited'] == theirs['visited']
+            assert mine['terminal'] == theirs['terminal']
+            assert set(mine['Q']) == set(theirs['Q'])
+            for fen in theirs['Q']:
+                assert mine['legal_moves'][fen] == list(theirs['legal_moves'][fen])
+                assert np.array_equal(mine['Q'][fen], theirs['Q'][fen]), fen
+                assert np.array_equal(mine['N'][fen], theirs['N'][fen]), fen
+                assert np.array_equal(mine['P'][fen], np.asarray(theirs['P'][fen], np.float32)), fen
+
+
+def test_numpy1_cast_mode_vs_oracle():
+    from oracle.mcts import SyntheticEvaluator
+    from oracle import selfplay
+    ev = SyntheticEvaluator(salt=5)
+    eng = _engine(2, 16, cast_mode=1)
+    recs, _ = drive_engine(eng, 2, 16, [7, 8], evaluator=ev)
+    for g, s in enumerate([7, 8]):
+        ref = selfplay.play_games(ev, 1, 16, seed_base=s, cast_mode=1)[0]
+        assert compare_records(recs[g], ref)[2] is None
+
+
+def test_host_torch_net_matches_reference_trace():
+    """L1 with the real network: leaves evaluated batch-1 on the CPU exactly like the
+    reference (exp/agent.py:67-69) -> the reference's own seed-0 game, bit-exact."""
+    from oracle.mcts import TorchNetEvaluator
+    from oracle.net import seed0_network
+    gm = load_golden('trees')['net_seed0'][0]
+    eng = _engine(1, gm['sims'])
+    recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=TorchNetEvaluator(seed0_network()))
+    assert compare_records(recs[0], gm['moves'])[2] is None
+
+
+def test_gpu_net_move_identity_vs_reference_trace(record_property):
+    """L3: the whole search on the GPU (network included) vs the reference trace."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    gm = load_golden('trees')['net_seed0'][0]
+    eng = _engine(1, gm['sims'])
+    torch.manual_seed(0)
+    eng.set_weights(Network())
+    recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=None)
+    same, total, first = compare_records(recs[0], gm['moves'])
+    record_property('move_identity', f'{same}/{total}')
+    print(f'GPU-net move identity vs reference: {same}/{total} (first divergence: {first})')
+    assert first is None or first >= 10
+
+
+def test_cpp_driver_equals_python_driver():
+    """mtaz_play (C++ host RNG + action choice) == the Python/numpy driver, same GPU net."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    seeds = [0, 1, 2, 3]
+    torch.manual_seed(0)
+    net = Network()
+    eng = _engine(len(seeds), 12, seed_base=0)
+    eng.set_weights(net)
+    eng.play()
+    got = eng.episodes()
+    eng2 = _engine(len(seeds), 12)
+    eng2.set_weights(net)
+    ref, _ = drive_engine(eng2, len(seeds), 12, seeds, evaluator=None)
+    for a, b in zip(got, ref):
+        assert compare_records(a, b)[2] is None
+        assert [r['reward'] for r in a] == [r['reward'] for r in b]
+
+
+def test_games_independent_of_batch_composition():
+    """Per-game results depend only on the game's seed (the multi-GPU sharding contract)."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    big = _engine(6, 8, seed_base=100)
+    big.set_weights(net)
+    big.play()
+    all_eps = big.episodes()
+    for g in (0, 3, 5):
+        one = _engine(1, 8, seed_base=100 + g)
+        one.set_weights(net)
+        one.play()
+        assert compare_records(one.episodes()[0], all_eps[g])[2] is None
