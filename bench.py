@@ -117,7 +117,7 @@ def main():
     # HIP events around the 18 trunk launches on the engine's stream.
     launches = 18 * tot['waves']
     conv_ms_avg = tot['trunk_ms'] / launches if launches else float('nan')
-    flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / launches if launches else float('nan')
+    flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
     achieved = flop_per_launch / (conv_ms_avg * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):

@@ -561,21 +561,31 @@ __global__ __launch_bounds__(256, 1) void k_conv3x3(const float* __restrict__ in
   const int b0 = blockIdx.x * 2;
   if (b0 >= nb) return;
   const int tid = threadIdx.x;
-  for (int i = tid; i < 2 * 256 * 56; i += 256) lds[i] = 0.f;
+  // stage: in[b][ci][0..31] as 8 float4 per (board, ci).  Thread tid owns float4 q = tid&7
+  // of channels ci = (tid>>3) + 32j, j = 0..7, for both boards: all 16 loads are issued
+  // before the first LDS write.
+  const int q = tid & 7, p0 = q * 4;
+  float4 st[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int bb = j >> 3, ci = (tid >> 3) + 32 * (j & 7);
+    st[j] = (b0 + bb < nb) ? reinterpret_cast<const float4*>(in + (size_t)(b0 + bb) * 8192 + ci * 32)[q]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  {
+    float4* l4 = reinterpret_cast<float4*>(lds);
+    for (int i = tid; i < 2 * 256 * 56 / 4; i += 256) l4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   __syncthreads();
-  // stage: in[b][ci][0..31] as 8 float4 per (board, ci)
-  for (int idx = tid; idx < 2 * 256 * 8; idx += 256) {
-    const int bb = idx >> 11, rem = idx & 2047, ci = rem >> 3, q = rem & 7;
-    const int b = b0 + bb;
-    if (b < nb) {
-      const float4 v = reinterpret_cast<const float4*>(in + (size_t)b * 8192 + ci * 32)[q];
-      float* dst = lds + (ci * 2 + bb) * 56;
-      const int p0 = q * 4;
-      if (p0 + 0 < 30) dst[padpos(p0 + 0)] = v.x;
-      if (p0 + 1 < 30) dst[padpos(p0 + 1)] = v.y;
-      if (p0 + 2 < 30) dst[padpos(p0 + 2)] = v.z;
-      if (p0 + 3 < 30) dst[padpos(p0 + 3)] = v.w;
-    }
+  const int pp0 = padpos(p0), pp1 = padpos(p0 + 1), pp2 = padpos(p0 + 2), pp3 = padpos(p0 + 3);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int bb = j >> 3, ci = (tid >> 3) + 32 * (j & 7);
+    float* dst = lds + (ci * 2 + bb) * 56;
+    dst[pp0] = st[j].x;
+    dst[pp1] = st[j].y;
+    if (p0 + 2 < 30) dst[pp2] = st[j].z;      // q = 7 covers positions 28..31 (30, 31 are padding)
+    if (p0 + 3 < 30) dst[pp3] = st[j].w;
   }
   __syncthreads();
 
@@ -585,39 +595,57 @@ __global__ __launch_bounds__(256, 1) void k_conv3x3(const float* __restrict__ in
   const float4* w0 = wpk + (size_t)(2 * wave) * 288 * 64 + lane;
   const float4* w1 = wpk + (size_t)(2 * wave + 1) * 288 * 64 + lane;
   f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
-  float4 nb0 = w0[0], nb1 = w1[0];
-  for (int tap = 0; tap < 9; ++tap) {
-    const int off = (tap / 3 - 1) * 7 + (tap % 3 - 1);
-    const float* abase = lds + kh * 112 + pp + off;
-    for (int q = 0; q < 32; ++q) {
-      const int s4 = tap * 32 + q;
-      const float4 cb0 = nb0, cb1 = nb1;
-      if (s4 + 1 < 288) {
-        nb0 = w0[(s4 + 1) * 64];
-        nb1 = w1[(s4 + 1) * 64];
-      }
-      const float* a = abase + q * 4 * 224;
-      const float a00 = a[0], a01 = a[56];
-      const float a10 = a[224], a11 = a[224 + 56];
-      const float a20 = a[448], a21 = a[448 + 56];
-      const float a30 = a[672], a31 = a[672 + 56];
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a00, cb0.x, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a00, cb1.x, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a01, cb0.x, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a01, cb1.x, acc11, 0, 0, 0);
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a10, cb0.y, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a10, cb1.y, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a11, cb0.y, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a11, cb1.y, acc11, 0, 0, 0);
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a20, cb0.z, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a20, cb1.z, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a21, cb0.z, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a21, cb1.z, acc11, 0, 0, 0);
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a30, cb0.w, acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a30, cb1.w, acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a31, cb0.w, acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a31, cb1.w, acc11, 0, 0, 0);
+  // Software pipeline over the 288 groups of 4 k-steps (k = tap*256 + ci): the weight
+  // float4s of group s+2 and the 8 A values of group s+1 are issued before the 16 MFMAs
+  // of group s; sched_barrier keeps the compiler from sinking them next to their use.
+  auto a_ptr = [&](int s4) {
+    const int tap = s4 >> 5, q = s4 & 31;
+    return lds + kh * 112 + pp + (tap / 3 - 1) * 7 + (tap % 3 - 1) + q * 4 * 224;
+  };
+  float4 wb0[2], wb1[2];
+  wb0[0] = w0[0];
+  wb1[0] = w1[0];
+  wb0[1] = w0[64];
+  wb1[1] = w1[64];
+  float an[8];
+  {
+    const float* a = a_ptr(0);
+    an[0] = a[0]; an[1] = a[56]; an[2] = a[224]; an[3] = a[280];
+    an[4] = a[448]; an[5] = a[504]; an[6] = a[672]; an[7] = a[728];
+  }
+#pragma unroll 2
+  for (int s4 = 0; s4 < 288; ++s4) {
+    const float4 cb0 = wb0[s4 & 1], cb1 = wb1[s4 & 1];
+    float ac[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ac[j] = an[j];
+    if (s4 + 2 < 288) {
+      wb0[s4 & 1] = w0[(s4 + 2) * 64];
+      wb1[s4 & 1] = w1[(s4 + 2) * 64];
     }
+    if (s4 + 1 < 288) {
+      const float* a = a_ptr(s4 + 1);
+      an[0] = a[0]; an[1] = a[56]; an[2] = a[224]; an[3] = a[280];
+      an[4] = a[448]; an[5] = a[504]; an[6] = a[672]; an[7] = a[728];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[0], cb0.x, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[0], cb1.x, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[1], cb0.x, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[1], cb1.x, acc11, 0, 0, 0);
+    acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[2], cb0.y, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[2], cb1.y, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[3], cb0.y, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[3], cb1.y, acc11, 0, 0, 0);
+    acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[4], cb0.z, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[4], cb1.z, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[5], cb0.z, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[5], cb1.z, acc11, 0, 0, 0);
+    acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[6], cb0.w, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[6], cb1.w, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[7], cb0.w, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[7], cb1.w, acc11, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
   // epilogue: col = lane&31 -> channel; rows (r&3) + 8(r>>2) + 4*kh -> positions
 #pragma unroll
