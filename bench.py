@@ -22,6 +22,7 @@ sys.path.insert(0, HERE)
 
 METRIC = 'self-play games/sec + MCTS sims/sec at 1/2/4/8 MI355X (fixed sims/move)'
 FP32_MATRIX_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md chip table (f32-input MFMA = f32 vector rate)
+F16_MATRIX_PEAK_TFLOPS = 2500.0      # dense f16/bf16 MFMA (MI355X_MICROARCH.md; sparsity figures excluded)
 
 
 def cpu_baseline(sims, threads, seconds_cap):
@@ -49,6 +50,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=0)
     ap.add_argument('--games', type=int, default=4096, help='parallel games per GPU (BASELINE config 2: 4096)')
     ap.add_argument('--sims', type=int, default=64, help='MCTS simulations per move (config 2: 64)')
+    ap.add_argument('--precision', default='f16x3', choices=['f16x3', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
@@ -79,6 +81,7 @@ def main():
     eng = Engine(n_games=G, sims=sims, device=device, seed_base=rank * G)
     torch.manual_seed(0)                      # random-init weights of the reference architecture
     eng.set_weights(Network())
+    eng.set_precision(args.precision)
     eng.set_timing(True)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
     for _ in range(args.warmup):
@@ -112,12 +115,22 @@ def main():
             dist.destroy_process_group()
         return
 
-    # roofline of the dominant kernel (k_conv3x3, 18 launches per simulation wave):
-    # algorithmic FLOP per launch = boards in the launch x 2*30*256*2304, duration from
-    # HIP events around the 18 trunk launches on the engine's stream.
-    launches = 18 * tot['waves']
+    # roofline of the dominant kernel, timed with HIP events on the engine's stream:
+    #  fp16x3 (default): k_net_x, ONE launch per simulation wave = the whole network on the
+    #    wave's leaves; algorithmic FLOP per launch = leaves x 638,245,892.
+    #    It runs on v_mfma_f32_32x32x16_f16, so the peak is the dense f16 MFMA rate; the 3
+    #    split passes mean issued MFMA FLOP = 3x the trunk's algorithmic FLOP.
+    #  fp32: k_conv3x3, 18 launches per wave; FLOP per launch = leaves x 2*30*256*2304.
+    f16x3 = st.get('net_precision', 0) == 1
+    if f16x3:
+        launches = tot['waves']
+        flop_per_launch = FLOP_PER_EVAL * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
+        kernel, peak = 'k_net_x (fused network, fp16x3 on MFMA 32x32x16 f16)', F16_MATRIX_PEAK_TFLOPS
+    else:
+        launches = 18 * tot['waves']
+        flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
+        kernel, peak = 'k_conv3x3 (fp32 MFMA 32x32x2)', FP32_MATRIX_PEAK_TFLOPS
     conv_ms_avg = tot['trunk_ms'] / launches if launches else float('nan')
-    flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
     achieved = flop_per_launch / (conv_ms_avg * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -138,7 +151,7 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'fp32',
+        'dtype': 'f16x3 (fp16 hi/lo split, fp32 accumulate; fp32-accurate)' if f16x3 else 'fp32',
         'data': 'synthetic: self-play from STARTING_FEN, random-init weights (torch.manual_seed(0); Network())',
         'config': {'workload': f'{G} parallel self-play games per GPU, {sims} sims/move, random-init policy net '
                                f'(BASELINE config 2; config 4 = 8 GPUs x 4096)',
@@ -150,9 +163,10 @@ def main():
         'terminal_sims_per_game': tot['terminal_sims'] / games,
         'decisive_games': int(tot['decisive']),
         'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12,
-        'roofline': {'bound': 'mfma', 'kernel': 'k_conv3x3 (fp32 MFMA 32x32x2)', 'achieved': achieved,
-                     'peak': FP32_MATRIX_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / FP32_MATRIX_PEAK_TFLOPS,
-                     'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch},
+        'roofline': {'bound': 'mfma', 'kernel': kernel, 'achieved': achieved,
+                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
+                     'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch,
+                     'mfma_passes': 3 if f16x3 else 1},
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
     }

@@ -107,8 +107,11 @@ int mtaz_records_get(mtaz_engine* h, uint32_t* pos, int32_t* action, int32_t* k,
                      float* reward, int32_t* outcome);
 /* counters of the last mtaz_play: see minitchess_alphazero_amd/engine.py STAT_NAMES */
 int mtaz_stats(mtaz_engine* h, double* out, int n);
-/* record per-wave trunk (18 conv launches) HIP events during mtaz_play */
+/* record per-wave network HIP events during mtaz_play (trunk span for fp32, the fused
+ * network kernel for fp16x3) */
 int mtaz_set_timing(mtaz_engine* h, int on);
+/* network arithmetic: 1 = fp16x3 split MFMA (default, fp32-accurate), 0 = fp32 MFMA */
+int mtaz_set_precision(mtaz_engine* h, int precision);
 
 /* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */

@@ -18,6 +18,7 @@ ARCH = os.environ.get('MTAZ_OFFLOAD_ARCH', 'gfx950')
 
 SOURCES = [
     ('mtaz_device.hip', ['-O3']),
+    ('mtaz_net.hip', ['-O3']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
 ]
 HEADERS = ['rules.h', 'engine.h']

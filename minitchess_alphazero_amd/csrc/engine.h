@@ -112,9 +112,18 @@ struct NetWeights {
   const float* vl1_b;     // [256]
   const float* vl2_w;     // [256]
   const float* vl2_b;     // [1]
+  // fp16x3 trunk (k_net_x): per layer the BN-folded weights scaled by 2^e_L and split
+  // hi = f16(w), lo = f16(w - hi), laid out as the A operand of v_mfma_f32_32x32x16_f16:
+  // [L 18][cotile 8][kblock 144][part hi/lo][lane 64][8 x f16]; lane l holds
+  // W[co = 32*cotile + (l&31)][k = 16*kblock + 8*(l>>5) + j], k = tap*256 + ci.
+  const uint4* convx;
+  const float* convx_inv; // [18] 2^-e_L
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
+constexpr size_t CONVX_U4_PER_LAYER = (size_t)8 * 144 * 2 * 64;  // 147,456 x 16 B = 2.36 MB
+enum NetPrecision { NET_FP32 = 0, NET_F16X3 = 1 };
+constexpr int ERR_F16 = 512;   // activation exceeded the f16 range in the fp16x3 trunk
 
 struct NetBuffers {
   float* x0;              // [B][256][32]
@@ -134,6 +143,9 @@ void launch_move_begin(const Dev& d, hipStream_t s);
 void launch_select(const Dev& d, int sim, hipStream_t s);
 void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const Pos* pos, const int32_t* count, int max_b,
                 int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end);
+// fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup)
+void launch_net_x(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end);
 void launch_backup(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);

@@ -427,7 +427,7 @@ struct PlyRec {
 
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
-  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_COUNT
+  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_COUNT
 };
 
 template <class F>
@@ -466,6 +466,9 @@ struct mtaz_engine {
   NetWeights w{};
   NetBuffers nb{};
   bool weights_ok = false;
+  int precision = NET_F16X3;
+  uint4* wxbuf = nullptr;
+  float* wxinv = nullptr;
   std::vector<void*> allocs;
   float* wbuf = nullptr;
   // scratch
@@ -652,6 +655,7 @@ static int check_err(mtaz_engine* h) {
     if (e & ERR_ILLEGAL) m += " illegal-action";
     if (e & ERR_HIST) m += " history-capacity";
     if (e & ERR_HASH) m += " hash-full";
+    if (e & ERR_F16) m += " activation-exceeds-f16-range";
     return set_err((e & ERR_ILLEGAL) ? MTAZ_E_ILLEGAL : MTAZ_E_CAPACITY, "device error flags 0x%x:%s", e, m.c_str());
   }
   return 0;
@@ -748,7 +752,60 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.vl1_b = b + o_v1b;
   h->w.vl2_w = b + o_v2w;
   h->w.vl2_b = b + o_v2b;
+
+  // fp16x3 trunk weights: per layer scale 2^e (max |w| * 2^e <= 8192), hi = f16(w),
+  // lo = f16(w - hi), in the A-operand order of v_mfma_f32_32x32x16_f16 (engine.h).
+  std::vector<_Float16> wx((size_t)CONV_LAYERS * CONVX_U4_PER_LAYER * 8);
+  std::vector<float> winv(CONV_LAYERS);
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const int base = 7 + L * 6;
+    fold(base, 256, sc, sh);
+    const std::vector<float>& W = t[base];
+    double mx = 0;
+    for (int co = 0; co < 256; ++co)
+      for (int j = 0; j < 256 * 9; ++j) mx = std::max(mx, fabs(W[(size_t)co * 2304 + j] * sc[co]));
+    const int e = mx > 0 ? (int)floor(log2(8192.0 / mx)) : 0;
+    const double s = ldexp(1.0, e);
+    winv[L] = (float)ldexp(1.0, -e);
+    _Float16* dst = wx.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    for (int ct = 0; ct < 8; ++ct)
+      for (int kb = 0; kb < 144; ++kb)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int co = ct * 32 + (lane & 31), k = kb * 16 + 8 * (lane >> 5) + j;
+            const int tap = k >> 8, ci = k & 255;
+            const double v = (double)W[((size_t)co * 256 + ci) * 9 + tap] * sc[co] * s;
+            const _Float16 hi = (_Float16)v;
+            const _Float16 lo = (_Float16)(v - (double)hi);
+            const size_t u4 = ((size_t)ct * 144 + kb) * 128 + lane;
+            dst[u4 * 8 + j] = hi;
+            dst[(u4 + 64) * 8 + j] = lo;
+          }
+  }
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, wx.size() / 8));
+  if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS));
+  HIPCHK(hipMemcpy(h->wxbuf, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxinv, winv.data(), CONV_LAYERS * 4, hipMemcpyHostToDevice));
+  h->w.convx = h->wxbuf;
+  h->w.convx_inv = h->wxinv;
   h->weights_ok = true;
+  return 0;
+}
+
+static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count, int max_b, int mode, float* logits,
+                           float* values, hipEvent_t eb, hipEvent_t ee) {
+  if (h->precision == NET_F16X3) {
+    launch_net_x(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee);
+  } else {
+    NetBuffers nb = h->nb;
+    nb.logits = logits;
+    launch_net(h->d, h->w, nb, pos, count, max_b, mode, values, h->stream, eb, ee);
+  }
+}
+
+extern "C" int mtaz_set_precision(mtaz_engine* h, int precision) {
+  if (precision != NET_FP32 && precision != NET_F16X3) return set_err(MTAZ_E_FAIL, "precision must be 0 (fp32) or 1 (fp16x3)");
+  h->precision = precision;
   return 0;
 }
 
@@ -757,14 +814,12 @@ extern "C" int mtaz_evaluate(mtaz_engine* h, const uint32_t* d_pos, int n, float
   HIPCHK(hipSetDevice(h->device));
   for (int s = 0; s < n; s += h->G) {
     const int m = std::min(h->G, n - s);
-    NetBuffers nb = h->nb;
-    nb.logits = d_logits + (size_t)s * NUM_ACTIONS;
-    launch_net(h->d, h->w, nb, reinterpret_cast<const Pos*>(d_pos) + s, nullptr, m, NET_FULL_LOGITS, d_values + s,
-               h->stream, nullptr, nullptr);
+    launch_network(h, reinterpret_cast<const Pos*>(d_pos) + s, nullptr, m, NET_FULL_LOGITS,
+                   d_logits + (size_t)s * NUM_ACTIONS, d_values + s, nullptr, nullptr);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipStreamSynchronize(h->stream));
-  return 0;
+  return check_err(h);
 }
 
 // ---- fine-grained search API ----------------------------------------------------------------
@@ -856,7 +911,7 @@ static int sim_gpu(mtaz_engine* h, int sim) {
     eb = h->ev[2 * h->wave];
     ee = h->ev[2 * h->wave + 1];
   }
-  launch_net(h->d, h->w, h->nb, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, h->stream, eb, ee);
+  launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, eb, ee);
   launch_backup(h->d, h->stream);
   if (h->wave < h->count_log_cap)
     HIPCHK(hipMemcpyAsync(h->d_count_log + h->wave, h->d.lf.count, 4, hipMemcpyDeviceToDevice, h->stream));
@@ -1110,6 +1165,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_TRUNK_LAUNCHES] = h->timing ? 18.0 * h->wave : 0;
   h->stats[ST_MAX_NODES] = mxn;
   h->stats[ST_SYNC_MS] = sync_ms;
+  h->stats[ST_NET_PREC] = h->precision;
   return 0;
 }
 

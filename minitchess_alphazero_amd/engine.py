@@ -23,7 +23,7 @@ from . import _lib
 from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_to_fen
 
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
-              'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms']
+              'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
@@ -85,6 +85,10 @@ class Engine:
         return logits.cpu().numpy(), values.cpu().numpy()
 
     # ---- batched self-play -----------------------------------------------------------------------
+    def set_precision(self, precision):
+        """'f16x3' (default: fp16 hi/lo split MFMA, fp32-accurate) or 'fp32' (fp32 MFMA)."""
+        _lib.check(self.L.mtaz_set_precision(self.h, {'fp32': 0, 'f16x3': 1}[precision]))
+
     def set_timing(self, on=True):
         self.L.mtaz_set_timing(self.h, 1 if on else 0)
 

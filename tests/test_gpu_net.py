@@ -23,12 +23,13 @@ def _softmax(x):
     return e / e.sum()
 
 
-@pytest.fixture(scope='module')
-def engine():
+@pytest.fixture(scope='module', params=['f16x3', 'fp32'])
+def engine(request):
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.network import Network
     import torch
     eng = Engine(n_games=64, sims=8)
+    eng.set_precision(request.param)
     torch.manual_seed(0)
     net = Network()
     eng.set_weights(net)
