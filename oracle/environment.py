@@ -1,10 +1,13 @@
-"""MinitChess environment / episode restatement (TEST INFRASTRUCTURE, see oracle/__init__.py).
+"""MinitChess environment restatement over oracle.rules (TEST INFRASTRUCTURE, see oracle/__init__.py).
 
-Restates exp/environment.py:1-91 over oracle.rules (the fork stand-in):
-  * _update_attributes: FEN observation, result -> (reward, done), legal move
-    codes SORTED with duplicates kept (:34-50)
-  * step: uci4 decode, retry with +'q' (queen promotion), else IlegalMove (:68-82)
-  * exceptions derive from BaseException (:8-13)
+Behaviour of exp/environment.py:1-91 that the tests pin:
+  * observation = 4-field FEN; result '1-0'/'0-1' -> reward 1.0, '1/2-1/2' -> 0.0,
+    done; an ongoing position leaves the previous reward untouched (:39-45, the `self_reward`
+    typo means _reward is only ever None or a terminal reward)
+  * legal moves = codes of m.uci()[:4], sorted, duplicates kept (:48-50)
+  * step: terminal -> TerminatedEpisodeStepException; decode the code, try the uci4 move,
+    then the queen promotion, else IlegalMoveException (:68-82)
+  * both exceptions derive from BaseException (:8-13)
 """
 from collections import namedtuple
 
@@ -15,9 +18,15 @@ STARTING_FEN = rules.STARTING_FEN
 
 EpisodeStatus = namedtuple('EpisodeStatus', ['observation', 'reward', 'done'])
 
-_MD = moves_dict()
-MOVES_DICT = {True: _MD['w'], False: _MD['b']}                                     # :16-18
-MOVES_DICT_INV = {side: {v: k for k, v in MOVES_DICT[side].items()} for side in (True, False)}  # :19
+
+def _side_tables():
+    md = moves_dict()
+    enc = {True: md['w'], False: md['b']}
+    dec = {side: {code: uci for uci, code in table.items()} for side, table in enc.items()}
+    return enc, dec
+
+
+MOVES_DICT, MOVES_DICT_INV = _side_tables()
 NUM_ACTIONS = len(MOVES_DICT[True])
 
 
@@ -29,25 +38,27 @@ class IlegalMoveException(BaseException):
     pass
 
 
+_RESULT_REWARD = {'1-0': 1.0, '0-1': 1.0, '1/2-1/2': 0.0}
+
+
 class MinitChessEpisode:
     def __init__(self, fen, board=None):
-        self._board = board if board is not None else rules.Board(fen)
+        self._board = rules.Board(fen) if board is None else board
         self._reward = None
         self._done = None
-        self._update_attributes()
+        self._refresh()
 
-    def _update_attributes(self):                                                  # :34-50
-        self._observation = self._board.fen()
-        res = self._board.result()
-        if res in ('1-0', '0-1'):
-            self._reward, self._done = 1., True
-        elif res == '1/2-1/2':
-            self._reward, self._done = 0., True
+    def _refresh(self):
+        b = self._board
+        self._observation = b.fen()
+        outcome = b.result()
+        if outcome in _RESULT_REWARD:
+            self._reward, self._done = _RESULT_REWARD[outcome], True
         else:
-            self._done = False          # NB the reference never resets _reward here (:45 typo)
-        self._legal_moves_uci = list(self._board.legal_moves)
-        side = MOVES_DICT[self.turn]
-        self._legal_moves = sorted(side[m.uci()[:4]] for m in self._legal_moves_uci)
+            self._done = False
+        self._moves = list(b.legal_moves)
+        table = MOVES_DICT[b.turn]
+        self._codes = sorted(table[m.uci()[:4]] for m in self._moves)
 
     def get_observation(self):
         return self._observation
@@ -59,7 +70,7 @@ class MinitChessEpisode:
         return self._done
 
     def get_legal_moves(self):
-        return self._legal_moves
+        return self._codes
 
     @property
     def turn(self):
@@ -69,25 +80,25 @@ class MinitChessEpisode:
     def board(self):
         return self._board
 
-    def step(self, action, return_status=True):                                   # :68-82
-        if self.is_done():
+    def step(self, action, return_status=True):
+        if self._done:
             raise TerminatedEpisodeStepException
-        uci = MOVES_DICT_INV[self.turn][action]
-        move = rules.Move.from_uci(uci)
-        if move not in self._legal_moves_uci:
-            move = rules.Move.from_uci(uci + 'q')
-        if move not in self._legal_moves_uci:
+        uci4 = MOVES_DICT_INV[self.turn][action]
+        for candidate in (uci4, uci4 + 'q'):
+            mv = rules.Move.from_uci(candidate)
+            if mv in self._moves:
+                break
+        else:
             raise IlegalMoveException
-        self._board.push(move)
-        self._update_attributes()
-        if return_status:
-            return self.get_status()
+        self._board.push(mv)
+        self._refresh()
+        return self.get_status() if return_status else None
 
     def get_status(self):
         return EpisodeStatus(self._observation, self._reward, self._done)
 
 
 class MinitChessEnvironment:
-    def new_episode(self, fen=None):                                               # :88-91
-        episode = MinitChessEpisode(fen or STARTING_FEN)
-        return episode, episode.get_observation()
+    def new_episode(self, fen=None):
+        ep = MinitChessEpisode(fen or STARTING_FEN)
+        return ep, ep.get_observation()
