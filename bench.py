@@ -77,8 +77,10 @@ def main():
     from minitchess_alphazero_amd.engine import Engine, FLOP_PER_CONV_BOARD, FLOP_PER_EVAL, start_position
     from minitchess_alphazero_amd.network import Network
 
+    from minitchess_alphazero_amd.sharding import reduce_run, shard
     G, sims = args.games, args.sims
-    eng = Engine(n_games=G, sims=sims, device=device, seed_base=rank * G)
+    seed_base, _ = shard(rank, world, G)
+    eng = Engine(n_games=G, sims=sims, device=device, seed_base=seed_base)
     torch.manual_seed(0)                      # random-init weights of the reference architecture
     eng.set_weights(Network())
     eng.set_precision(args.precision)
@@ -102,13 +104,7 @@ def main():
             tot[k] += st[k]
     sync()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=torch.device('cuda', device))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        s = torch.tensor([tot[k] for k in tot], dtype=torch.float64, device=torch.device('cuda', device))
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        tot = dict(zip(tot, s.tolist()))
+    dt, tot = reduce_run(dt, tot, dist, torch.device('cuda', device))
     games = G * args.steps * world
     if rank != 0:
         if dist is not None:

@@ -112,6 +112,8 @@ int mtaz_stats(mtaz_engine* h, double* out, int n);
 int mtaz_set_timing(mtaz_engine* h, int on);
 /* network arithmetic: 1 = fp16x3 split MFMA (default, fp32-accurate), 0 = fp32 MFMA */
 int mtaz_set_precision(mtaz_engine* h, int precision);
+/* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
+int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
 
 /* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */

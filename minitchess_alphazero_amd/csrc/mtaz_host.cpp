@@ -803,6 +803,11 @@ static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count,
   }
 }
 
+extern "C" int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base) {
+  h->seed_base = seed_base;
+  return 0;
+}
+
 extern "C" int mtaz_set_precision(mtaz_engine* h, int precision) {
   if (precision != NET_FP32 && precision != NET_F16X3) return set_err(MTAZ_E_FAIL, "precision must be 0 (fp32) or 1 (fp16x3)");
   h->precision = precision;

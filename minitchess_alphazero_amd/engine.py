@@ -89,6 +89,10 @@ class Engine:
         """'f16x3' (default: fp16 hi/lo split MFMA, fp32-accurate) or 'fp32' (fp32 MFMA)."""
         _lib.check(self.L.mtaz_set_precision(self.h, {'fp32': 0, 'f16x3': 1}[precision]))
 
+    def set_seed_base(self, seed_base):
+        """Game slot g of the next play() uses np.random.seed(seed_base + g) semantics."""
+        _lib.check(self.L.mtaz_set_seed_base(self.h, int(seed_base)))
+
     def set_timing(self, on=True):
         self.L.mtaz_set_timing(self.h, 1 if on else 0)
 
