@@ -114,6 +114,11 @@ int mtaz_set_timing(mtaz_engine* h, int on);
 int mtaz_set_precision(mtaz_engine* h, int precision);
 /* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
 int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
+/* network-only timing harness: avg ms over `iters` launches on n device positions; with
+ * stamped != 0 also per-workgroup phase cycles [nwg][stem, conv K loops, epilogues, heads]
+ * from a separate diagnostic build (tools/bench_net.py) */
+int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int stamped, float* ms_out,
+                  uint64_t* stamps_out);
 
 /* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */

@@ -803,6 +803,46 @@ static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count,
   }
 }
 
+// Kernel timing harness for the network alone (tools/bench_net.py): `iters` back-to-back
+// full-logit launches on n device positions timed with HIP events; optionally one more
+// launch of the stamp-instrumented diagnostic build (phase cycle shares per workgroup).
+extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int stamped, float* ms_out,
+                             uint64_t* stamps_out) {
+  if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
+  if (n <= 0 || iters <= 0) return set_err(MTAZ_E_FAIL, "n and iters must be positive");
+  HIPCHK(hipSetDevice(h->device));
+  float *logits = nullptr, *values = nullptr;
+  unsigned long long* st = nullptr;
+  const int nwg = (n + 3) / 4;
+  HIPCHK(hipMalloc(&logits, (size_t)n * NUM_ACTIONS * 4));
+  HIPCHK(hipMalloc(&values, (size_t)n * 4));
+  HIPCHK(hipMalloc(&st, (size_t)nwg * 4 * 8));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  const Pos* pos = reinterpret_cast<const Pos*>(d_pos);
+  if (h->precision == NET_FP32 && n > h->G) return set_err(MTAZ_E_CAPACITY, "fp32 path: n must be <= engine games");
+  launch_network(h, pos, nullptr, n, NET_FULL_LOGITS, logits, values, nullptr, nullptr);   // warm-up
+  HIPCHK(hipEventRecord(e0, h->stream));
+  for (int i = 0; i < iters; ++i) launch_network(h, pos, nullptr, n, NET_FULL_LOGITS, logits, values, nullptr, nullptr);
+  HIPCHK(hipEventRecord(e1, h->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  *ms_out = ms / iters;
+  if (stamped && stamps_out) {
+    launch_net_x_stamped(h->d, h->w, pos, n, logits, values, st, h->stream);
+    HIPCHK(hipMemcpyAsync(stamps_out, st, (size_t)nwg * 4 * 8, hipMemcpyDeviceToHost, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(logits);
+  (void)hipFree(values);
+  (void)hipFree(st);
+  return check_err(h);
+}
+
 extern "C" int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base) {
   h->seed_base = seed_base;
   return 0;

@@ -46,15 +46,28 @@ __device__ __forceinline__ int src_row(int col, int ph, int pw, int tap) {
 
 __device__ __forceinline__ int padpos_x(int p) { return (p / 5 + 1) * 7 + (p % 5 + 1); }
 
+// STAMP = diagnostic build only: thread 0 accumulates s_memtime deltas per phase
+// (stem, conv K loops, conv epilogues, heads) into stamps[block*4 + phase].
+template <bool STAMP>
 __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
-                                                  float* __restrict__ logits_out, float* __restrict__ values_out) {
+                                                  float* __restrict__ logits_out, float* __restrict__ values_out,
+                                                  unsigned long long* __restrict__ stamps) {
   __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
   if (b0 >= nb) return;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, col = lane & 31, h = lane >> 5;
+  unsigned long long t_prev = 0, st_stem = 0, st_k = 0, st_epi = 0, st_heads = 0;
+  if constexpr (STAMP) t_prev = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](unsigned long long& acc) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - t_prev;
+      t_prev = t;
+    }
+  };
 
   // ---------------- stem: tokens -> Embedding(7,4) -> conv3x3 8->256 + BN + ReLU ----------
   float* xin = reinterpret_cast<float*>(smem + IMGB);          // [bb][8][56] fp32, zero padded
@@ -111,6 +124,7 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   }
   __syncthreads();
 
+  stamp(st_stem);
   // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
   const int ph = col / 5, pw = col % 5;
   f32x16x acc[8];
@@ -175,6 +189,7 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
 #undef MMA
 #undef LOAD_B
 #undef LOAD_A
+    stamp(st_k);
     __syncthreads();   // every wave has finished reading this layer's input image
 
     // epilogue: y = ReLU(acc * 2^-e + bias) (conv B: acc already holds 2^e * x, the residual)
@@ -223,6 +238,7 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
       for (int i = 0; i < 8; ++i) acc[i] = (f32x16x){0};
     }
     __syncthreads();
+    stamp(st_epi);
   }
   if (overflow) atomicOr(D.pr.err, ERR_F16);
 
@@ -265,6 +281,15 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
 #pragma unroll
       for (int bb = 0; bb < XB; ++bb) red[bb * 256 + tid] += red[bb * 256 + tid + s];
     __syncthreads();
+  }
+  stamp(st_heads);
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      stamps[blockIdx.x * 4 + 0] = st_stem;
+      stamps[blockIdx.x * 4 + 1] = st_k;
+      stamps[blockIdx.x * 4 + 2] = st_epi;
+      stamps[blockIdx.x * 4 + 3] = st_heads;
+    }
   }
   // wave bb finishes board bb: value, then policy logits / legal softmax
   const int bb = wave;
@@ -322,9 +347,16 @@ void launch_net_x(const Dev& d, const NetWeights& w, const Pos* pos, const int32
                   float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end) {
   if (max_b <= 0) return;
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
-  hipLaunchKernelGGL(k_net_x, dim3((max_b + XB - 1) / XB), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
-                     values_out);
+  hipLaunchKernelGGL(k_net_x<false>, dim3((max_b + XB - 1) / XB), dim3(256), 0, s, d, w, pos, count, max_b, mode,
+                     logits_out, values_out, (unsigned long long*)nullptr);
   if (ev_end) (void)hipEventRecord(ev_end, s);
+}
+
+void launch_net_x_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                          float* values_out, unsigned long long* stamps, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_net_x<true>, dim3((n + XB - 1) / XB), dim3(256), 0, s, d, w, pos, (const int32_t*)nullptr, n,
+                     (int)NET_FULL_LOGITS, logits_out, values_out, stamps);
 }
 
 }  // namespace mtaz
