@@ -118,6 +118,11 @@ struct NetWeights {
   // W[co = 32*cotile + (l&31)][k = 16*kblock + 8*(l>>5) + j], k = tap*256 + ci.
   const uint4* convx;
   const float* convx_inv; // [18] 2^-e_L
+  // stem in the same form: K = 5 k-blocks of (2 taps x 8 channels), tap 9 = zero:
+  // [cotile 8][kblock 5][part][lane 64][8 x f16], lane l: co = 32*cotile + (l&31),
+  // tap = 2*kblock + (l>>5), channel j
+  const uint4* stemx;
+  const float* stemx_inv; // [1]
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304

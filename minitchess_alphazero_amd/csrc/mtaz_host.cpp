@@ -782,12 +782,38 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             dst[(u4 + 64) * 8 + j] = lo;
           }
   }
-  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, wx.size() / 8));
-  if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS));
+  // stem (tensor 1: [256][8][3][3]) in the same split form, 5 k-blocks of 2 taps x 8 channels
+  std::vector<_Float16> sx((size_t)8 * 5 * 128 * 8);
+  {
+    fold(1, 256, sc, sh);
+    double mx = 0;
+    for (int co = 0; co < 256; ++co)
+      for (int j = 0; j < 72; ++j) mx = std::max(mx, fabs(t[1][co * 72 + j] * sc[co]));
+    const int e = mx > 0 ? (int)floor(log2(8192.0 / mx)) : 0;
+    const double s = ldexp(1.0, e);
+    winv.push_back((float)ldexp(1.0, -e));
+    for (int ct = 0; ct < 8; ++ct)
+      for (int kb = 0; kb < 5; ++kb)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int co = ct * 32 + (lane & 31), tap = 2 * kb + (lane >> 5), c = j;
+            const double v = tap < 9 ? (double)t[1][co * 72 + c * 9 + tap] * sc[co] * s : 0.0;
+            const _Float16 hi = (_Float16)v;
+            const _Float16 lo = (_Float16)(v - (double)hi);
+            const size_t u4 = ((size_t)ct * 5 + kb) * 128 + lane;
+            sx[u4 * 8 + j] = hi;
+            sx[(u4 + 64) * 8 + j] = lo;
+          }
+  }
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, wx.size() / 8 + sx.size() / 8));
+  if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
   HIPCHK(hipMemcpy(h->wxbuf, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxinv, winv.data(), CONV_LAYERS * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + wx.size() / 8, sx.data(), sx.size() * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx = h->wxbuf;
   h->w.convx_inv = h->wxinv;
+  h->w.stemx = h->wxbuf + wx.size() / 8;
+  h->w.stemx_inv = h->wxinv + CONV_LAYERS;
   h->weights_ok = true;
   return 0;
 }

@@ -46,6 +46,22 @@ __device__ __forceinline__ int src_row(int col, int ph, int pw, int tap) {
 
 __device__ __forceinline__ int padpos_x(int p) { return (p / 5 + 1) * 7 + (p % 5 + 1); }
 
+// Three split passes Wh*Xh + Wh*Xl + Wl*Xh over the wave's 8 tiles (2 channel tiles x
+// XB boards); SA = {ct0 hi, ct0 lo, ct1 hi, ct1 lo}, SB = {bb0 hi, bb0 lo, ...}.  Pass-major
+// order keeps 7 independent MFMAs between two updates of one accumulator.
+#define MMA3(SA, SB)                                                                                  \
+  {                                                                                                   \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                               \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
+      acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_], SB[2 * bb_], acc[ct_ * 4 + bb_], 0, 0, 0); \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                               \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
+      acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_], SB[2 * bb_ + 1], acc[ct_ * 4 + bb_], 0, 0, 0); \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                               \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
+      acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_ + 1], SB[2 * bb_], acc[ct_ * 4 + bb_], 0, 0, 0); \
+  }
+
 // STAMP = diagnostic build only: thread 0 accumulates s_memtime deltas per phase
 // (stem, conv K loops, conv epilogues, heads) into stamps[block*4 + phase].
 template <bool STAMP>
@@ -69,134 +85,16 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
     }
   };
 
-  // ---------------- stem: tokens -> Embedding(7,4) -> conv3x3 8->256 + BN + ReLU ----------
-  float* xin = reinterpret_cast<float*>(smem + IMGB);          // [bb][8][56] fp32, zero padded
-  for (int i = tid; i < XB * 8 * 56; i += 256) xin[i] = 0.f;
-  for (int i = tid; i < 2 * XB * 32; i += 256) {
-    const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
-    *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  if (tid < XB * 30) {
-    const int bb = tid / 30, i = tid % 30;          // i = square index in the mover's view
-    const int b = b0 + bb;
-    int own = 0, opp = 0;
-    if (b < nb) {
-      const BB bd = unpack(pos[b]);
-      const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
-      const int t = piece_type_at(bd, s);
-      const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
-      own = mine ? token_code(t) : 0;
-      opp = (t && !mine) ? token_code(t) : 0;
-    }
-    float* xb = xin + bb * 8 * 56;
-    const int pp = padpos_x(i);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      xb[e * 56 + pp] = W.emb[own * 4 + e];
-      xb[(4 + e) * 56 + pp] = W.emb[opp * 4 + e];
-    }
-  }
-  __syncthreads();
-  {
-    const int co = tid;
-    float w[72];
-#pragma unroll
-    for (int j = 0; j < 72; ++j) w[j] = W.stem_w[co * 72 + j];
-    const float bias = W.stem_b[co];
-    for (int bb = 0; bb < XB; ++bb) {
-      const float* xb = xin + bb * 8 * 56;
-      for (int p = 0; p < 30; ++p) {
-        const int pp = padpos_x(p);
-        float acc = bias;
-#pragma unroll
-        for (int ci = 0; ci < 8; ++ci)
-#pragma unroll
-          for (int tap = 0; tap < 9; ++tap) acc += w[ci * 9 + tap] * xb[ci * 56 + pp + (tap / 3 - 1) * 7 + (tap % 3 - 1)];
-        const float y = fmaxf(acc, 0.f);
-        const _Float16 hi = (_Float16)y;
-        const _Float16 lo = (_Float16)(y - (float)hi);
-        const int byte = (co & 7) * 2;
-        *reinterpret_cast<_Float16*>(smem + ioff(0, bb, p, co >> 3) + byte) = hi;
-        *reinterpret_cast<_Float16*>(smem + ioff(1, bb, p, co >> 3) + byte) = lo;
-      }
-    }
-  }
-  __syncthreads();
-
-  stamp(st_stem);
-  // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
   const int ph = col / 5, pw = col % 5;
   f32x16x acc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = (f32x16x){0};
   int overflow = 0;
 
-  for (int L = 0; L < CONV_LAYERS; ++L) {
-    const uint4* Wl = W.convx + (size_t)L * CONVX_U4_PER_LAYER + (size_t)(2 * wave) * KBLK * 2 * 64 + lane;
-    f16x8 A0[4], A1[4], A2[4], B0[8], B1[8];
-#define LOAD_A(S, KB)                                                                 \
-    {                                                                                 \
-      const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                  \
-      const uint4* p_ = Wl + (size_t)kk_ * 128;                                       \
-      S[0] = __builtin_bit_cast(f16x8, p_[0]);                                        \
-      S[1] = __builtin_bit_cast(f16x8, p_[64]);                                       \
-      S[2] = __builtin_bit_cast(f16x8, p_[KBLK * 128]);                               \
-      S[3] = __builtin_bit_cast(f16x8, p_[KBLK * 128 + 64]);                          \
-    }
-#define LOAD_B(S, KB)                                                                 \
-    {                                                                                 \
-      const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                  \
-      const int src_ = src_row(col, ph, pw, kk_ >> 4);                                \
-      const int off_ = src_ * RB + (((2 * (kk_ & 15) + h) ^ (src_ & 15)) << 4);       \
-      _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                          \
-        S[2 * bb_] = *reinterpret_cast<const f16x8*>(smem + bb_ * IROWS * RB + off_); \
-        S[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(smem + PARTB + bb_ * IROWS * RB + off_); \
-      }                                                                               \
-    }
-#define MMA(SA, SB)                                                                                   \
-    {                                                                                                 \
-      _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                             \
-      _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                            \
-        acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_], SB[2 * bb_], acc[ct_ * 4 + bb_], 0, 0, 0); \
-      _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                             \
-      _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                            \
-        acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_], SB[2 * bb_ + 1], acc[ct_ * 4 + bb_], 0, 0, 0); \
-      _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                             \
-      _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                            \
-        acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_ + 1], SB[2 * bb_], acc[ct_ * 4 + bb_], 0, 0, 0); \
-    }
-#define STEP(KB, AC, AP, BC, BP)          \
-    {                                     \
-      LOAD_A(AP, (KB) + 2);               \
-      LOAD_B(BP, (KB) + 1);               \
-      __builtin_amdgcn_sched_barrier(0);  \
-      MMA(AC, BC);                        \
-      __builtin_amdgcn_sched_barrier(0);  \
-    }
-    LOAD_A(A0, 0);
-    LOAD_A(A1, 1);
-    LOAD_B(B0, 0);
-    for (int kb = 0; kb < KBLK; kb += 6) {
-      STEP(kb + 0, A0, A2, B0, B1);
-      STEP(kb + 1, A1, A0, B1, B0);
-      STEP(kb + 2, A2, A1, B0, B1);
-      STEP(kb + 3, A0, A2, B1, B0);
-      STEP(kb + 4, A1, A0, B0, B1);
-      STEP(kb + 5, A2, A1, B1, B0);
-    }
-#undef STEP
-#undef MMA
-#undef LOAD_B
-#undef LOAD_A
-    stamp(st_k);
-    __syncthreads();   // every wave has finished reading this layer's input image
-
-    // epilogue: y = ReLU(acc * 2^-e + bias) (conv B: acc already holds 2^e * x, the residual)
-    const bool conv_a = (L & 1) == 0;
-    const float inv = W.convx_inv[L];
-    const float s_next = conv_a ? 1.0f / W.convx_inv[L + 1] : 0.f;
-    const float* bias = W.conv_b + L * 256;
+  // Epilogue of every conv (and the stem): y = ReLU(acc * 2^-e + bias) written in place as
+  // f16 hi/lo.  conv_a: the image still holds the block input x -> seed the next conv's
+  // accumulators with 2^e_next * x (the residual of conv B); otherwise reset them.
+  auto epilogue = [&](float inv, const float* bias, bool conv_a, float s_next) {
     if (col < 30) {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
@@ -237,6 +135,117 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = (f32x16x){0};
     }
+  };
+
+  // ---------------- stem: tokens -> Embedding(7,4) -> conv3x3 8->256 + BN + ReLU ----------
+  // Same implicit GEMM on f16 MFMA with K = 5 k-blocks of (2 taps x 8 channels); the input
+  // image [part][board][row][8 ch] f16 (rows = squares in the mover's view + zero row)
+  // sits in the aux region.
+  char* simg = smem + IMGB;
+  for (int i = tid; i < 2 * XB * IROWS; i += 256) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 2 * XB * 32; i += 256) {
+    const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
+    *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  if (tid < XB * 30) {
+    const int bb = tid / 30, i = tid % 30;          // i = square index in the mover's view
+    const int b = b0 + bb;
+    int own = 0, opp = 0;
+    if (b < nb) {
+      const BB bd = unpack(pos[b]);
+      const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
+      const int t = piece_type_at(bd, s);
+      const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
+      own = mine ? token_code(t) : 0;
+      opp = (t && !mine) ? token_code(t) : 0;
+    }
+    f16x8 xh, xl;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {                   // channel c = plane*4 + e (exp/policy.py:73-74)
+      const float v = W.emb[(c < 4 ? own : opp) * 4 + (c & 3)];
+      xh[c] = (_Float16)v;
+      xl[c] = (_Float16)(v - (float)xh[c]);
+    }
+    *reinterpret_cast<f16x8*>(simg + (bb * IROWS + i) * 16) = xh;
+    *reinterpret_cast<f16x8*>(simg + ((XB + bb) * IROWS + i) * 16) = xl;
+  }
+  __syncthreads();
+  {
+    const uint4* Ws = W.stemx + (size_t)(2 * wave) * 5 * 128 + lane;
+    for (int kb = 0; kb < 5; ++kb) {
+      f16x8 SA[4], SB[8];
+      const uint4* p = Ws + kb * 128;
+      SA[0] = __builtin_bit_cast(f16x8, p[0]);
+      SA[1] = __builtin_bit_cast(f16x8, p[64]);
+      SA[2] = __builtin_bit_cast(f16x8, p[5 * 128]);
+      SA[3] = __builtin_bit_cast(f16x8, p[5 * 128 + 64]);
+      const int tap = 2 * kb + h;
+      const int src = tap < 9 ? src_row(col, ph, pw, tap) : ZROW;
+#pragma unroll
+      for (int bb = 0; bb < XB; ++bb) {
+        SB[2 * bb] = *reinterpret_cast<const f16x8*>(simg + (bb * IROWS + src) * 16);
+        SB[2 * bb + 1] = *reinterpret_cast<const f16x8*>(simg + ((XB + bb) * IROWS + src) * 16);
+      }
+      MMA3(SA, SB);
+    }
+  }
+  epilogue(W.stemx_inv[0], W.stem_b, false, 0.f);
+  __syncthreads();
+
+  stamp(st_stem);
+  // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
+
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const uint4* Wl = W.convx + (size_t)L * CONVX_U4_PER_LAYER + (size_t)(2 * wave) * KBLK * 2 * 64 + lane;
+    f16x8 A0[4], A1[4], A2[4], B0[8], B1[8];
+#define LOAD_A(S, KB)                                                                 \
+    {                                                                                 \
+      const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                  \
+      const uint4* p_ = Wl + (size_t)kk_ * 128;                                       \
+      S[0] = __builtin_bit_cast(f16x8, p_[0]);                                        \
+      S[1] = __builtin_bit_cast(f16x8, p_[64]);                                       \
+      S[2] = __builtin_bit_cast(f16x8, p_[KBLK * 128]);                               \
+      S[3] = __builtin_bit_cast(f16x8, p_[KBLK * 128 + 64]);                          \
+    }
+#define LOAD_B(S, KB)                                                                 \
+    {                                                                                 \
+      const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                  \
+      const int src_ = src_row(col, ph, pw, kk_ >> 4);                                \
+      const int off_ = src_ * RB + (((2 * (kk_ & 15) + h) ^ (src_ & 15)) << 4);       \
+      _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                          \
+        S[2 * bb_] = *reinterpret_cast<const f16x8*>(smem + bb_ * IROWS * RB + off_); \
+        S[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(smem + PARTB + bb_ * IROWS * RB + off_); \
+      }                                                                               \
+    }
+#define STEP(KB, AC, AP, BC, BP)          \
+    {                                     \
+      LOAD_A(AP, (KB) + 2);               \
+      LOAD_B(BP, (KB) + 1);               \
+      __builtin_amdgcn_sched_barrier(0);  \
+      MMA3(AC, BC);                       \
+      __builtin_amdgcn_sched_barrier(0);  \
+    }
+    LOAD_A(A0, 0);
+    LOAD_A(A1, 1);
+    LOAD_B(B0, 0);
+    for (int kb = 0; kb < KBLK; kb += 6) {
+      STEP(kb + 0, A0, A2, B0, B1);
+      STEP(kb + 1, A1, A0, B1, B0);
+      STEP(kb + 2, A2, A1, B0, B1);
+      STEP(kb + 3, A0, A2, B1, B0);
+      STEP(kb + 4, A1, A0, B0, B1);
+      STEP(kb + 5, A2, A1, B1, B0);
+    }
+#undef STEP
+#undef LOAD_B
+#undef LOAD_A
+    stamp(st_k);
+    __syncthreads();   // every wave has finished reading this layer's input image
+
+    // epilogue: y = ReLU(acc * 2^-e + bias) (conv B: acc already holds 2^e * x, the residual)
+    const bool conv_a = (L & 1) == 0;
+    epilogue(W.convx_inv[L], W.conv_b + L * 256, conv_a, conv_a ? 1.0f / W.convx_inv[L + 1] : 0.f);
     __syncthreads();
     stamp(st_epi);
   }
