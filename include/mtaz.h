@@ -115,10 +115,12 @@ int mtaz_set_precision(mtaz_engine* h, int precision);
 /* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
 int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
 /* network-only timing harness: avg ms over `iters` launches on n device positions; with
- * stamped != 0 also per-workgroup phase cycles [nwg][stem, conv K loops, epilogues, heads]
- * from a separate diagnostic build (tools/bench_net.py) */
+ * stamped != 0 also per-workgroup [nwg][stem, conv K loops, epilogues, heads cycles, total
+ * cycles, total 100 MHz ticks] from a separate diagnostic build (tools/bench_net.py) */
 int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int stamped, float* ms_out,
                   uint64_t* stamps_out);
+/* select a k_net_x code variant for A/B timing (0 = the product kernel) */
+int mtaz_set_net_variant(mtaz_engine* h, int variant);
 
 /* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */

@@ -150,10 +150,11 @@ void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const P
                 int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end);
 // fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup)
 void launch_net_x(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
-                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end);
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                  int variant = 0);
 // diagnostic instantiation with per-phase s_memtime stamps (never the product path)
 void launch_net_x_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
-                          float* values_out, unsigned long long* stamps, hipStream_t s);
+                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant = 0);
 void launch_backup(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);

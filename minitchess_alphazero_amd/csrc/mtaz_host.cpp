@@ -467,6 +467,7 @@ struct mtaz_engine {
   NetBuffers nb{};
   bool weights_ok = false;
   int precision = NET_F16X3;
+  int variant = 0;   // k_net_x A/B variant (0 = product kernel)
   uint4* wxbuf = nullptr;
   float* wxinv = nullptr;
   std::vector<void*> allocs;
@@ -821,7 +822,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
 static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count, int max_b, int mode, float* logits,
                            float* values, hipEvent_t eb, hipEvent_t ee) {
   if (h->precision == NET_F16X3) {
-    launch_net_x(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee);
+    launch_net_x(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee, h->variant);
   } else {
     NetBuffers nb = h->nb;
     nb.logits = logits;
@@ -840,9 +841,10 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   float *logits = nullptr, *values = nullptr;
   unsigned long long* st = nullptr;
   const int nwg = (n + 3) / 4;
+  const int NST = 6;
   HIPCHK(hipMalloc(&logits, (size_t)n * NUM_ACTIONS * 4));
   HIPCHK(hipMalloc(&values, (size_t)n * 4));
-  HIPCHK(hipMalloc(&st, (size_t)nwg * 4 * 8));
+  HIPCHK(hipMalloc(&st, (size_t)nwg * NST * 8));
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
@@ -857,8 +859,8 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
   *ms_out = ms / iters;
   if (stamped && stamps_out) {
-    launch_net_x_stamped(h->d, h->w, pos, n, logits, values, st, h->stream);
-    HIPCHK(hipMemcpyAsync(stamps_out, st, (size_t)nwg * 4 * 8, hipMemcpyDeviceToHost, h->stream));
+    launch_net_x_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
+    HIPCHK(hipMemcpyAsync(stamps_out, st, (size_t)nwg * NST * 8, hipMemcpyDeviceToHost, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
   (void)hipEventDestroy(e0);
@@ -867,6 +869,11 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   (void)hipFree(values);
   (void)hipFree(st);
   return check_err(h);
+}
+
+extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
+  h->variant = variant;
+  return 0;
 }
 
 extern "C" int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base) {

@@ -64,7 +64,9 @@ __device__ __forceinline__ int padpos_x(int p) { return (p / 5 + 1) * 7 + (p % 5
 
 // STAMP = diagnostic build only: thread 0 accumulates s_memtime deltas per phase
 // (stem, conv K loops, conv epilogues, heads) into stamps[block*4 + phase].
-template <bool STAMP>
+// VAR: variant bits for in-process A/B timing (tools/bench_net.py); 0 = the product kernel.
+//   bit 0: stem on the VALU in fp32 instead of the f16 MFMA split
+template <bool STAMP, int VAR>
 __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
                                                   float* __restrict__ logits_out, float* __restrict__ values_out,
@@ -76,7 +78,11 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, col = lane & 31, h = lane >> 5;
   unsigned long long t_prev = 0, st_stem = 0, st_k = 0, st_epi = 0, st_heads = 0;
-  if constexpr (STAMP) t_prev = __builtin_amdgcn_s_memtime();
+  unsigned long long t_start = 0, r_start = 0;
+  if constexpr (STAMP) {
+    t_prev = t_start = __builtin_amdgcn_s_memtime();
+    r_start = __builtin_amdgcn_s_memrealtime();
+  }
   auto stamp = [&](unsigned long long& acc) {
     if constexpr (STAMP) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -142,11 +148,59 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   // image [part][board][row][8 ch] f16 (rows = squares in the mover's view + zero row)
   // sits in the aux region.
   char* simg = smem + IMGB;
-  for (int i = tid; i < 2 * XB * IROWS; i += 256) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
   for (int i = tid; i < 2 * XB * 32; i += 256) {
     const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
     *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
   }
+  if constexpr (VAR & 1) {
+    // A/B variant: fp32 VALU stem, thread = output channel
+    float* xin = reinterpret_cast<float*>(simg);          // [bb][8][56] fp32, zero padded
+    for (int i = tid; i < XB * 8 * 56; i += 256) xin[i] = 0.f;
+    __syncthreads();
+    if (tid < XB * 30) {
+      const int bb = tid / 30, i = tid % 30;
+      const int b = b0 + bb;
+      int own = 0, opp = 0;
+      if (b < nb) {
+        const BB bd = unpack(pos[b]);
+        const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
+        const int t = piece_type_at(bd, s);
+        const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
+        own = mine ? token_code(t) : 0;
+        opp = (t && !mine) ? token_code(t) : 0;
+      }
+      const int pp = padpos_x(i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xin[bb * 448 + e * 56 + pp] = W.emb[own * 4 + e];
+        xin[bb * 448 + (4 + e) * 56 + pp] = W.emb[opp * 4 + e];
+      }
+    }
+    __syncthreads();
+    const int co = tid;
+    float w[72];
+#pragma unroll
+    for (int j = 0; j < 72; ++j) w[j] = W.stem_w[co * 72 + j];
+    const float bias = W.stem_b[co];
+    for (int bb = 0; bb < XB; ++bb) {
+      const float* xb = xin + bb * 448;
+      for (int p = 0; p < 30; ++p) {
+        const int pp = padpos_x(p);
+        float a = bias;
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci)
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) a += w[ci * 9 + tap] * xb[ci * 56 + pp + (tap / 3 - 1) * 7 + (tap % 3 - 1)];
+        const float y = fmaxf(a, 0.f);
+        const _Float16 hi = (_Float16)y;
+        const _Float16 lo = (_Float16)(y - (float)hi);
+        *reinterpret_cast<_Float16*>(smem + ioff(0, bb, p, co >> 3) + (co & 7) * 2) = hi;
+        *reinterpret_cast<_Float16*>(smem + ioff(1, bb, p, co >> 3) + (co & 7) * 2) = lo;
+      }
+    }
+    __syncthreads();
+  } else {
+  for (int i = tid; i < 2 * XB * IROWS; i += 256) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
   if (tid < XB * 30) {
     const int bb = tid / 30, i = tid % 30;          // i = square index in the mover's view
@@ -192,6 +246,7 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   }
   epilogue(W.stemx_inv[0], W.stem_b, false, 0.f);
   __syncthreads();
+  }
 
   stamp(st_stem);
   // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
@@ -294,10 +349,12 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
-      stamps[blockIdx.x * 4 + 0] = st_stem;
-      stamps[blockIdx.x * 4 + 1] = st_k;
-      stamps[blockIdx.x * 4 + 2] = st_epi;
-      stamps[blockIdx.x * 4 + 3] = st_heads;
+      stamps[blockIdx.x * 6 + 0] = st_stem;
+      stamps[blockIdx.x * 6 + 1] = st_k;
+      stamps[blockIdx.x * 6 + 2] = st_epi;
+      stamps[blockIdx.x * 6 + 3] = st_heads;
+      stamps[blockIdx.x * 6 + 4] = __builtin_amdgcn_s_memtime() - t_start;      // shader cycles
+      stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;  // 100 MHz ticks
     }
   }
   // wave bb finishes board bb: value, then policy logits / legal softmax
@@ -352,20 +409,34 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   }
 }
 
+template <bool S>
+static void launch_variant(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
+                           const int32_t* count, int max_b, int mode, float* logits, float* values,
+                           unsigned long long* stamps) {
+  switch (var) {
+    case 1:
+      hipLaunchKernelGGL((k_net_x<S, 1>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+      break;
+    default:
+      hipLaunchKernelGGL((k_net_x<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  }
+}
+
 void launch_net_x(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
-                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end) {
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                  int variant) {
   if (max_b <= 0) return;
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
-  hipLaunchKernelGGL(k_net_x<false>, dim3((max_b + XB - 1) / XB), dim3(256), 0, s, d, w, pos, count, max_b, mode,
-                     logits_out, values_out, (unsigned long long*)nullptr);
+  launch_variant<false>(variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode, logits_out, values_out,
+                        nullptr);
   if (ev_end) (void)hipEventRecord(ev_end, s);
 }
 
 void launch_net_x_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
-                          float* values_out, unsigned long long* stamps, hipStream_t s) {
+                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_net_x<true>, dim3((n + XB - 1) / XB), dim3(256), 0, s, d, w, pos, (const int32_t*)nullptr, n,
-                     (int)NET_FULL_LOGITS, logits_out, values_out, stamps);
+  launch_variant<true>(variant, dim3((n + XB - 1) / XB), s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS, logits_out,
+                       values_out, stamps);
 }
 
 }  // namespace mtaz

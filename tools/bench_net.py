@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""Network-only microbenchmark (k_net_x / fp32 path) on n random positions.
+"""Network-only microbenchmark and in-process A/B of k_net_x code variants.
 
-Prints the average launch time (HIP events, back-to-back launches), the algorithmic
-TFLOP/s (638,245,892 FLOP per board) and, from one launch of the stamp-instrumented
-diagnostic build, the per-workgroup cycle shares of stem / conv K loops / conv
-epilogues / heads.  Shares only: the stamped build itself is never timed.
+For each variant (interleaved over --rounds, one process, one device; MI355X devices
+clock ~10% apart, so only same-process comparisons mean anything):
+  * ms: average launch time over --iters back-to-back launches (HIP events)
+  * tflops_algorithmic: 638,245,892 FLOP per board / ms
+  * from one launch of the stamp-instrumented diagnostic build (shares only, never
+    timed): mean per-workgroup cycles, phase shares (stem / conv K loops / conv
+    epilogues / heads) and the effective clock (s_memtime / s_memrealtime).
 """
 import argparse
 import ctypes
@@ -14,14 +17,17 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests'))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--n', type=int, default=4096)
     ap.add_argument('--iters', type=int, default=10)
+    ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--variants', default='0')
     ap.add_argument('--precision', default='f16x3')
     args = ap.parse_args()
     import torch
@@ -38,19 +44,30 @@ def main():
     eng.set_precision(args.precision)
     d = torch.from_numpy(pos.view(np.int32)).cuda()
     torch.cuda.synchronize()
-    ms = ctypes.c_float()
+    variants = [int(v) for v in args.variants.split(',')]
     nwg = (args.n + 3) // 4
-    st = np.zeros(nwg * 4, np.uint64)
-    _lib.check(eng.L.mtaz_net_time(eng.h, ctypes.c_void_p(d.data_ptr()), args.n, args.iters, 1,
-                                   ctypes.byref(ms), st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
-    st = st.reshape(nwg, 4).astype(np.float64)
-    tot = st.sum(axis=1)
-    shares = (st / tot[:, None]).mean(axis=0)
-    out = {'n': args.n, 'precision': args.precision, 'ms': ms.value,
-           'tflops_algorithmic': FLOP_PER_EVAL * args.n / (ms.value * 1e-3) / 1e12,
-           'wg_cycles_mean': float(tot.mean()),
-           'shares': dict(zip(['stem', 'conv_kloop', 'conv_epilogue', 'heads'], shares.round(4).tolist()))}
-    print(json.dumps(out))
+    res = {v: {'ms': [], 'cycles': [], 'ghz': [], 'shares': []} for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            _lib.check(eng.L.mtaz_set_net_variant(eng.h, v))
+            ms = ctypes.c_float()
+            st = np.zeros(nwg * 6, np.uint64)
+            _lib.check(eng.L.mtaz_net_time(eng.h, ctypes.c_void_p(d.data_ptr()), args.n, args.iters, 1,
+                                           ctypes.byref(ms), st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+            st = st.reshape(nwg, 6).astype(np.float64)
+            res[v]['ms'].append(ms.value)
+            res[v]['cycles'].append(float(st[:, 4].mean()))
+            res[v]['ghz'].append(float((st[:, 4] / (st[:, 5] * 10.0)).mean()))   # cycles / (ticks * 10 ns) -> GHz
+            res[v]['shares'].append((st[:, :4] / st[:, :4].sum(axis=1, keepdims=True)).mean(axis=0))
+    for v in variants:
+        r = res[v]
+        ms = float(np.median(r['ms']))
+        out = {'variant': v, 'n': args.n, 'precision': args.precision, 'ms_median': ms, 'ms_all': r['ms'],
+               'tflops_algorithmic': FLOP_PER_EVAL * args.n / (ms * 1e-3) / 1e12,
+               'wg_cycles': float(np.median(r['cycles'])), 'clock_ghz_stamped': float(np.median(r['ghz'])),
+               'shares': dict(zip(['stem', 'conv_kloop', 'conv_epilogue', 'heads'],
+                                  np.mean(r['shares'], axis=0).round(4).tolist()))}
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == '__main__':
