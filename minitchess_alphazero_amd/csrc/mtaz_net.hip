@@ -62,6 +62,14 @@ __device__ __forceinline__ int padpos_x(int p) { return (p / 5 + 1) * 7 + (p % 5
       acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_ + 1], SB[2 * bb_], acc[ct_ * 4 + bb_], 0, 0, 0); \
   }
 
+// one split pass (8 MFMAs): W part WP (0 hi / 1 lo) x X part XP
+#define MMA_PASS(SA, SB, WP, XP)                                                                      \
+  {                                                                                                   \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                               \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
+      acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_ + (WP)], SB[2 * bb_ + (XP)], acc[ct_ * 4 + bb_], 0, 0, 0); \
+  }
+
 // STAMP = diagnostic build only: thread 0 accumulates s_memtime deltas per phase
 // (stem, conv K loops, conv epilogues, heads) into stamps[block*4 + phase].
 // VAR: variant bits for in-process A/B timing (tools/bench_net.py); 0 = the product kernel.
@@ -273,13 +281,37 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
         S[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(smem + PARTB + bb_ * IROWS * RB + off_); \
       }                                                                               \
     }
-#define STEP(KB, AC, AP, BC, BP)          \
-    {                                     \
-      LOAD_A(AP, (KB) + 2);               \
-      LOAD_B(BP, (KB) + 1);               \
-      __builtin_amdgcn_sched_barrier(0);  \
-      MMA3(AC, BC);                       \
-      __builtin_amdgcn_sched_barrier(0);  \
+#define STEP(KB, AC, AP, BC, BP)                  \
+    if constexpr (VAR & 8) {                      \
+      LOAD_A(AP, (KB) + 2);                       \
+      LOAD_B(BP, (KB) + 1);                       \
+      MMA3(AC, BC);                               \
+      _Pragma("unroll") for (int g_ = 0; g_ < 4; ++g_) {           \
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         \
+      }                                                            \
+      _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {           \
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         \
+      }                                                            \
+      __builtin_amdgcn_sched_barrier(0);          \
+    } else if constexpr (VAR & 2) {               \
+      MMA_PASS(AC, BC, 0, 0);                     \
+      __builtin_amdgcn_sched_barrier(0);          \
+      LOAD_A(AP, (KB) + 2);                       \
+      __builtin_amdgcn_sched_barrier(0);          \
+      MMA_PASS(AC, BC, 0, 1);                     \
+      __builtin_amdgcn_sched_barrier(0);          \
+      LOAD_B(BP, (KB) + 1);                       \
+      __builtin_amdgcn_sched_barrier(0);          \
+      MMA_PASS(AC, BC, 1, 0);                     \
+      __builtin_amdgcn_sched_barrier(0);          \
+    } else {                                      \
+      LOAD_A(AP, (KB) + 2);                       \
+      LOAD_B(BP, (KB) + 1);                       \
+      __builtin_amdgcn_sched_barrier(0);          \
+      MMA3(AC, BC);                               \
+      __builtin_amdgcn_sched_barrier(0);          \
     }
     LOAD_A(A0, 0);
     LOAD_A(A1, 1);
@@ -414,9 +446,15 @@ static void launch_variant(int var, dim3 grid, hipStream_t s, const Dev& d, cons
                            const int32_t* count, int max_b, int mode, float* logits, float* values,
                            unsigned long long* stamps) {
   switch (var) {
-    case 1:
-      hipLaunchKernelGGL((k_net_x<S, 1>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+#define MTAZ_VAR_CASE(V)                                                                                    \
+    case V:                                                                                                   \
+      hipLaunchKernelGGL((k_net_x<S, V>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, \
+                         stamps);                                                                             \
       break;
+    MTAZ_VAR_CASE(1)
+    MTAZ_VAR_CASE(2)
+    MTAZ_VAR_CASE(8)
+#undef MTAZ_VAR_CASE
     default:
       hipLaunchKernelGGL((k_net_x<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   }
