@@ -112,16 +112,16 @@ def main():
         return
 
     # roofline of the dominant kernel, timed with HIP events on the engine's stream:
-    #  fp16x3 (default): k_net_x, ONE launch per simulation wave = the whole network on the
+    #  fp16x3 (default): k_net_y, ONE launch per simulation wave = the whole network on the
     #    wave's leaves; algorithmic FLOP per launch = leaves x 638,245,892.
-    #    It runs on v_mfma_f32_32x32x16_f16, so the peak is the dense f16 MFMA rate; the 3
+    #    It runs on v_mfma_f32_16x16x32_f16, so the peak is the dense f16 MFMA rate; the 3
     #    split passes mean issued MFMA FLOP = 3x the trunk's algorithmic FLOP.
     #  fp32: k_conv3x3, 18 launches per wave; FLOP per launch = leaves x 2*30*256*2304.
     f16x3 = st.get('net_precision', 0) == 1
     if f16x3:
         launches = tot['waves']
         flop_per_launch = FLOP_PER_EVAL * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
-        kernel, peak = 'k_net_x (fused network, fp16x3 on MFMA 32x32x16 f16)', F16_MATRIX_PEAK_TFLOPS
+        kernel, peak = 'k_net_y (fused network, fp16x3 on MFMA 16x16x32 f16)', F16_MATRIX_PEAK_TFLOPS
     else:
         launches = 18 * tot['waves']
         flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')

@@ -19,9 +19,10 @@ ARCH = os.environ.get('MTAZ_OFFLOAD_ARCH', 'gfx950')
 SOURCES = [
     ('mtaz_device.hip', ['-O3']),
     ('mtaz_net.hip', ['-O3']),
+    ('mtaz_net16.hip', ['-O3']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
 ]
-HEADERS = ['rules.h', 'engine.h']
+HEADERS = ['rules.h', 'engine.h', 'net_common.h']
 
 
 def _hipcc():

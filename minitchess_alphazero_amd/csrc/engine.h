@@ -123,6 +123,13 @@ struct NetWeights {
   // tap = 2*kblock + (l>>5), channel j
   const uint4* stemx;
   const float* stemx_inv; // [1]
+  // the same split weights as the A operand of v_mfma_f32_16x16x32_f16 (k_net_y, product):
+  // [L 18][cotile 16][kblock 72][part][lane 64][8 x f16], lane l holds
+  // W[co = 16*cotile + (l&15)][k = 32*kblock + 8*(l>>4) + j]; scales as convx_inv
+  const uint4* convy;
+  // stem: [cotile 16][kblock 3][part][lane 64][8 x f16], co = 16*cotile + (l&15),
+  // tap = 4*kblock + (l>>4) (taps 9..11 zero), channel j; scale stemx_inv
+  const uint4* stemy;
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
@@ -148,13 +155,22 @@ void launch_move_begin(const Dev& d, hipStream_t s);
 void launch_select(const Dev& d, int sim, hipStream_t s);
 void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const Pos* pos, const int32_t* count, int max_b,
                 int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end);
-// fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup)
-void launch_net_x(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
-                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
-                  int variant = 0);
+// fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup).
+// Product kernel: k_net_y on v_mfma_f32_16x16x32_f16 (mtaz_net16.hip).  Variant bit
+// NET_VAR_X selects k_net_x on v_mfma_f32_32x32x16_f16 (mtaz_net.hip); the low bits pick
+// A/B schedules of either kernel (tools/bench_net.py).
+constexpr int NET_VAR_X = 512;
+void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                      float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                      int variant);
 // diagnostic instantiation with per-phase s_memtime stamps (never the product path)
-void launch_net_x_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
-                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant = 0);
+void launch_net_f16x3_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                              float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
+void launch_net_y(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                  int variant);
+void launch_net_y_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
 void launch_backup(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);

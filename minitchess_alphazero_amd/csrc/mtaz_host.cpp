@@ -467,7 +467,7 @@ struct mtaz_engine {
   NetBuffers nb{};
   bool weights_ok = false;
   int precision = NET_F16X3;
-  int variant = 0;   // k_net_x A/B variant (0 = product kernel)
+  int variant = 0;   // fp16x3 network kernel variant (0 = product k_net_y; NET_VAR_X = k_net_x)
   uint4* wxbuf = nullptr;
   float* wxinv = nullptr;
   std::vector<void*> allocs;
@@ -806,15 +806,50 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             sx[(u4 + 64) * 8 + j] = lo;
           }
   }
-  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, wx.size() / 8 + sx.size() / 8));
+  // the same split values re-laid out as the A operand of v_mfma_f32_16x16x32_f16 (k_net_y)
+  std::vector<_Float16> wy(wx.size());
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const _Float16* src = wx.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    _Float16* dst = wy.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    for (int ct = 0; ct < 16; ++ct)
+      for (int kb = 0; kb < 72; ++kb)
+        for (int part = 0; part < 2; ++part)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+              const int co = 16 * ct + (lane & 15), k = 32 * kb + 8 * (lane >> 4) + j;
+              // position of (co, k) in the 32x32x16 layout: cotile co/32, kblock k/16, lane (co%32) + 32*((k%16)/8)
+              const size_t xu4 = ((size_t)(co >> 5) * 144 + (k >> 4)) * 128 + part * 64 + (co & 31) + 32 * ((k & 15) >> 3);
+              dst[((((size_t)ct * 72 + kb) * 2 + part) * 64 + lane) * 8 + j] = src[xu4 * 8 + (k & 7)];
+            }
+  }
+  std::vector<_Float16> sy((size_t)16 * 3 * 128 * 8);
+  for (int ct = 0; ct < 16; ++ct)
+    for (int kb = 0; kb < 3; ++kb)
+      for (int part = 0; part < 2; ++part)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int co = 16 * ct + (lane & 15), tap = 4 * kb + (lane >> 4);
+            _Float16 v = (_Float16)0.f;
+            if (tap < 9) {   // stemx: cotile co/32, kblock tap/2, lane (co%32) + 32*(tap%2)
+              const size_t xu4 = ((size_t)(co >> 5) * 5 + (tap >> 1)) * 128 + part * 64 + (co & 31) + 32 * (tap & 1);
+              v = sx[xu4 * 8 + j];
+            }
+            sy[((((size_t)ct * 3 + kb) * 2 + part) * 64 + lane) * 8 + j] = v;
+          }
+  const size_t nx = wx.size() / 8, ns = sx.size() / 8, nsy = sy.size() / 8;
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, 2 * nx + ns + nsy));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
-  HIPCHK(hipMemcpy(h->wxbuf, wx.data(), wx.size() * 2, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + wx.size() / 8, sx.data(), sx.size() * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf, wx.data(), nx * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + nx, sx.data(), ns * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + nx + ns, wy.data(), nx * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns, sy.data(), nsy * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx = h->wxbuf;
   h->w.convx_inv = h->wxinv;
-  h->w.stemx = h->wxbuf + wx.size() / 8;
+  h->w.stemx = h->wxbuf + nx;
   h->w.stemx_inv = h->wxinv + CONV_LAYERS;
+  h->w.convy = h->wxbuf + nx + ns;
+  h->w.stemy = h->wxbuf + 2 * nx + ns;
   h->weights_ok = true;
   return 0;
 }
@@ -822,7 +857,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
 static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count, int max_b, int mode, float* logits,
                            float* values, hipEvent_t eb, hipEvent_t ee) {
   if (h->precision == NET_F16X3) {
-    launch_net_x(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee, h->variant);
+    launch_net_f16x3(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee, h->variant);
   } else {
     NetBuffers nb = h->nb;
     nb.logits = logits;
@@ -859,7 +894,7 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
   *ms_out = ms / iters;
   if (stamped && stamps_out) {
-    launch_net_x_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
+    launch_net_f16x3_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
     HIPCHK(hipMemcpyAsync(stamps_out, st, (size_t)nwg * NST * 8, hipMemcpyDeviceToHost, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));

@@ -16,35 +16,15 @@
 // ahead with ds_read_b128 on an XOR-swizzled image (conflict-free).  Residual
 // blocks: the conv-A epilogue reads the block input x and seeds the conv-B
 // accumulators with 2^e_B * x, so no extra residual buffer exists.
-#include "engine.h"
+#include <type_traits>
+
+#include "net_common.h"
 
 namespace mtaz {
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+using namespace netc;
 typedef float f32x16x __attribute__((ext_vector_type(16)));
-
-constexpr int XB = 4;                     // boards per workgroup
-constexpr int IROWS = 31;                 // image rows: squares 0..29 + zero row
-constexpr int ZROW = 30;
-constexpr int RB = 512;                   // bytes per row: 256 channels x f16
-constexpr int PARTB = XB * IROWS * RB;    // 63,488 B per part
-constexpr int IMGB = 2 * PARTB;           // 126,976 B
-constexpr int AUXB = XB * 8 * 56 * 4;     // 7,168 B: stem input / head features
 constexpr int KBLK = 144;                 // 2304 / 16
-
-__device__ __forceinline__ int ioff(int part, int bb, int row, int chunk) {
-  return part * PARTB + (bb * IROWS + row) * RB + ((chunk ^ (row & 15)) << 4);
-}
-
-// image row holding the source square of output square `col` for tap (dh, dw), or the zero row
-__device__ __forceinline__ int src_row(int col, int ph, int pw, int tap) {
-  const int dh = tap / 3 - 1, dw = tap - 3 * (tap / 3) - 1;
-  const int r = ph + dh, c = pw + dw;
-  return (col < 30 && r >= 0 && r < 6 && c >= 0 && c < 5) ? col + 5 * dh + dw : ZROW;
-}
-
-__device__ __forceinline__ int padpos_x(int p) { return (p / 5 + 1) * 7 + (p % 5 + 1); }
 
 // Three split passes Wh*Xh + Wh*Xl + Wl*Xh over the wave's 8 tiles (2 channel tiles x
 // XB boards); SA = {ct0 hi, ct0 lo, ct1 hi, ct1 lo}, SB = {bb0 hi, bb0 lo, ...}.  Pass-major
@@ -62,18 +42,11 @@ __device__ __forceinline__ int padpos_x(int p) { return (p / 5 + 1) * 7 + (p % 5
       acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_ + 1], SB[2 * bb_], acc[ct_ * 4 + bb_], 0, 0, 0); \
   }
 
-// one split pass (8 MFMAs): W part WP (0 hi / 1 lo) x X part XP
-#define MMA_PASS(SA, SB, WP, XP)                                                                      \
-  {                                                                                                   \
-    _Pragma("unroll") for (int ct_ = 0; ct_ < 2; ++ct_)                                               \
-    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
-      acc[ct_ * 4 + bb_] = __builtin_amdgcn_mfma_f32_32x32x16_f16(SA[2 * ct_ + (WP)], SB[2 * bb_ + (XP)], acc[ct_ * 4 + bb_], 0, 0, 0); \
-  }
-
 // STAMP = diagnostic build only: thread 0 accumulates s_memtime deltas per phase
 // (stem, conv K loops, conv epilogues, heads) into stamps[block*4 + phase].
-// VAR: variant bits for in-process A/B timing (tools/bench_net.py); 0 = the product kernel.
-//   bit 0: stem on the VALU in fp32 instead of the f16 MFMA split
+// VAR: variant bits for in-process A/B timing (tools/bench_net.py); 0 = its best schedule.
+// k_net_x is the A/B reference for the product kernel k_net_y (mtaz_net16.hip): same
+// algorithm on v_mfma_f32_32x32x16_f16, selected by variant bit NET_VAR_X.
 template <bool STAMP, int VAR>
 __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
@@ -108,8 +81,14 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   // Epilogue of every conv (and the stem): y = ReLU(acc * 2^-e + bias) written in place as
   // f16 hi/lo.  conv_a: the image still holds the block input x -> seed the next conv's
   // accumulators with 2^e_next * x (the residual of conv B); otherwise reset them.
-  auto epilogue = [&](float inv, const float* bias, bool conv_a, float s_next) {
+  // conv_a is a compile-time flag (std::true_type / false_type) so the conv-A and conv-B
+  // epilogues are two straight-line bodies.  The residual seed xh*s + xl*s and the lo part
+  // fma(hi, -1, y) are exact in fp32 (s is a power of two; y - hi is representable), so
+  // the stored values are the same bits as the unfused expressions.
+  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next) {
+    constexpr bool conv_a = decltype(conv_a_t)::value;
     if (col < 30) {
+      float ymax = 0.f;
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -121,15 +100,15 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
             f32x16x& a = acc[ct * 4 + bb];
             const int ah = ioff(0, bb, col, co0 >> 3) + 8 * h, al = ioff(1, bb, col, co0 >> 3) + 8 * h;
             float y[4];
-            y[0] = fmaxf(a[4 * g + 0] * inv + bv.x, 0.f);
-            y[1] = fmaxf(a[4 * g + 1] * inv + bv.y, 0.f);
-            y[2] = fmaxf(a[4 * g + 2] * inv + bv.z, 0.f);
-            y[3] = fmaxf(a[4 * g + 3] * inv + bv.w, 0.f);
-            if (conv_a) {
+            y[0] = fmaxf(__builtin_fmaf(a[4 * g + 0], inv, bv.x), 0.f);
+            y[1] = fmaxf(__builtin_fmaf(a[4 * g + 1], inv, bv.y), 0.f);
+            y[2] = fmaxf(__builtin_fmaf(a[4 * g + 2], inv, bv.z), 0.f);
+            y[3] = fmaxf(__builtin_fmaf(a[4 * g + 3], inv, bv.w), 0.f);
+            if constexpr (conv_a) {
               const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
               const f16x4 xl = *reinterpret_cast<const f16x4*>(smem + al);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) a[4 * g + j] = ((float)xh[j] + (float)xl[j]) * s_next;
+              for (int j = 0; j < 4; ++j) a[4 * g + j] = __builtin_fmaf((float)xh[j], s_next, (float)xl[j] * s_next);
             } else {
 #pragma unroll
               for (int j = 0; j < 4; ++j) a[4 * g + j] = 0.f;
@@ -137,14 +116,15 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
             f16x4 yh, yl;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              overflow |= y[j] >= 65504.f;
+              ymax = fmaxf(ymax, y[j]);
               yh[j] = (_Float16)y[j];
-              yl[j] = (_Float16)(y[j] - (float)yh[j]);
+              yl[j] = (_Float16)__builtin_fmaf((float)yh[j], -1.f, y[j]);
             }
             *reinterpret_cast<f16x4*>(smem + ah) = yh;
             *reinterpret_cast<f16x4*>(smem + al) = yl;
           }
         }
+      overflow |= ymax >= 65504.f;
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = (f32x16x){0};
@@ -156,82 +136,7 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
   // image [part][board][row][8 ch] f16 (rows = squares in the mover's view + zero row)
   // sits in the aux region.
   char* simg = smem + IMGB;
-  for (int i = tid; i < 2 * XB * 32; i += 256) {
-    const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
-    *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
-  }
-  if constexpr (VAR & 1) {
-    // A/B variant: fp32 VALU stem, thread = output channel
-    float* xin = reinterpret_cast<float*>(simg);          // [bb][8][56] fp32, zero padded
-    for (int i = tid; i < XB * 8 * 56; i += 256) xin[i] = 0.f;
-    __syncthreads();
-    if (tid < XB * 30) {
-      const int bb = tid / 30, i = tid % 30;
-      const int b = b0 + bb;
-      int own = 0, opp = 0;
-      if (b < nb) {
-        const BB bd = unpack(pos[b]);
-        const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
-        const int t = piece_type_at(bd, s);
-        const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
-        own = mine ? token_code(t) : 0;
-        opp = (t && !mine) ? token_code(t) : 0;
-      }
-      const int pp = padpos_x(i);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xin[bb * 448 + e * 56 + pp] = W.emb[own * 4 + e];
-        xin[bb * 448 + (4 + e) * 56 + pp] = W.emb[opp * 4 + e];
-      }
-    }
-    __syncthreads();
-    const int co = tid;
-    float w[72];
-#pragma unroll
-    for (int j = 0; j < 72; ++j) w[j] = W.stem_w[co * 72 + j];
-    const float bias = W.stem_b[co];
-    for (int bb = 0; bb < XB; ++bb) {
-      const float* xb = xin + bb * 448;
-      for (int p = 0; p < 30; ++p) {
-        const int pp = padpos_x(p);
-        float a = bias;
-#pragma unroll
-        for (int ci = 0; ci < 8; ++ci)
-#pragma unroll
-          for (int tap = 0; tap < 9; ++tap) a += w[ci * 9 + tap] * xb[ci * 56 + pp + (tap / 3 - 1) * 7 + (tap % 3 - 1)];
-        const float y = fmaxf(a, 0.f);
-        const _Float16 hi = (_Float16)y;
-        const _Float16 lo = (_Float16)(y - (float)hi);
-        *reinterpret_cast<_Float16*>(smem + ioff(0, bb, p, co >> 3) + (co & 7) * 2) = hi;
-        *reinterpret_cast<_Float16*>(smem + ioff(1, bb, p, co >> 3) + (co & 7) * 2) = lo;
-      }
-    }
-    __syncthreads();
-  } else {
-  for (int i = tid; i < 2 * XB * IROWS; i += 256) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  if (tid < XB * 30) {
-    const int bb = tid / 30, i = tid % 30;          // i = square index in the mover's view
-    const int b = b0 + bb;
-    int own = 0, opp = 0;
-    if (b < nb) {
-      const BB bd = unpack(pos[b]);
-      const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
-      const int t = piece_type_at(bd, s);
-      const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
-      own = mine ? token_code(t) : 0;
-      opp = (t && !mine) ? token_code(t) : 0;
-    }
-    f16x8 xh, xl;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {                   // channel c = plane*4 + e (exp/policy.py:73-74)
-      const float v = W.emb[(c < 4 ? own : opp) * 4 + (c & 3)];
-      xh[c] = (_Float16)v;
-      xl[c] = (_Float16)(v - (float)xh[c]);
-    }
-    *reinterpret_cast<f16x8*>(simg + (bb * IROWS + i) * 16) = xh;
-    *reinterpret_cast<f16x8*>(simg + ((XB + bb) * IROWS + i) * 16) = xl;
-  }
+  stem_input(smem, simg, pos, b0, nb, W, tid);
   __syncthreads();
   {
     const uint4* Ws = W.stemx + (size_t)(2 * wave) * 5 * 128 + lane;
@@ -252,132 +157,103 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
       MMA3(SA, SB);
     }
   }
-  epilogue(W.stemx_inv[0], W.stem_b, false, 0.f);
+  epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f);
   __syncthreads();
-  }
 
   stamp(st_stem);
   // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
 
-  for (int L = 0; L < CONV_LAYERS; ++L) {
-    const uint4* Wl = W.convx + (size_t)L * CONVX_U4_PER_LAYER + (size_t)(2 * wave) * KBLK * 2 * 64 + lane;
-    f16x8 A0[4], A1[4], A2[4], B0[8], B1[8];
+  // Weights stream from L2 through a ring of RS register slots PD k-blocks ahead of their
+  // use; activation fragments come from LDS one k-block ahead.
+  constexpr int PD = 2, RS = 3, U = 6;                   // U: unroll, a multiple of RS and of 2
+  static_assert(KBLK % U == 0 && U % RS == 0 && RS > PD, "ring");
+  f16x8 A[RS][4], B[2][8];
+  const uint4* Wl = W.convx + (size_t)(2 * wave) * KBLK * 2 * 64 + lane;
 #define LOAD_A(S, KB)                                                                 \
-    {                                                                                 \
-      const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                  \
-      const uint4* p_ = Wl + (size_t)kk_ * 128;                                       \
-      S[0] = __builtin_bit_cast(f16x8, p_[0]);                                        \
-      S[1] = __builtin_bit_cast(f16x8, p_[64]);                                       \
-      S[2] = __builtin_bit_cast(f16x8, p_[KBLK * 128]);                               \
-      S[3] = __builtin_bit_cast(f16x8, p_[KBLK * 128 + 64]);                          \
-    }
+  {                                                                                   \
+    const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                    \
+    const uint4* p_ = Wl + (size_t)kk_ * 128;                                         \
+    S[0] = __builtin_bit_cast(f16x8, p_[0]);                                          \
+    S[1] = __builtin_bit_cast(f16x8, p_[64]);                                         \
+    S[2] = __builtin_bit_cast(f16x8, p_[KBLK * 128]);                                 \
+    S[3] = __builtin_bit_cast(f16x8, p_[KBLK * 128 + 64]);                            \
+  }
 #define LOAD_B(S, KB)                                                                 \
-    {                                                                                 \
-      const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                  \
-      const int src_ = src_row(col, ph, pw, kk_ >> 4);                                \
-      const int off_ = src_ * RB + (((2 * (kk_ & 15) + h) ^ (src_ & 15)) << 4);       \
-      _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                          \
-        S[2 * bb_] = *reinterpret_cast<const f16x8*>(smem + bb_ * IROWS * RB + off_); \
-        S[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(smem + PARTB + bb_ * IROWS * RB + off_); \
-      }                                                                               \
-    }
+  {                                                                                   \
+    const int kk_ = (KB) < KBLK ? (KB) : KBLK - 1;                                    \
+    const int src_ = src_row(col, ph, pw, kk_ >> 4);                                  \
+    const int off_ = src_ * RB + (((2 * (kk_ & 15) + h) ^ (src_ & 15)) << 4);         \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                              \
+      S[2 * bb_] = *reinterpret_cast<const f16x8*>(smem + bb_ * IROWS * RB + off_);   \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                              \
+      S[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(smem + PARTB + bb_ * IROWS * RB + off_); \
+  }
+// Product schedule: the 24 MFMAs of a step interleaved with its loads by
+// sched_group_barrier (2 MFMA : 1 global load x4, then 2 MFMA : 1 ds_read x8), so the
+// loads issue in the MFMA shadow.  Variants: 128 = the next k-block's LDS reads first, in
+// consumption order, one per MFMA; 4 = all loads first, then the 24 MFMAs (first schedule).
 #define STEP(KB, AC, AP, BC, BP)                  \
-    if constexpr (VAR & 8) {                      \
-      LOAD_A(AP, (KB) + 2);                       \
-      LOAD_B(BP, (KB) + 1);                       \
-      MMA3(AC, BC);                               \
-      _Pragma("unroll") for (int g_ = 0; g_ < 4; ++g_) {           \
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         \
-      }                                                            \
-      _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {           \
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         \
-      }                                                            \
-      __builtin_amdgcn_sched_barrier(0);          \
-    } else if constexpr (VAR & 2) {               \
-      MMA_PASS(AC, BC, 0, 0);                     \
-      __builtin_amdgcn_sched_barrier(0);          \
-      LOAD_A(AP, (KB) + 2);                       \
-      __builtin_amdgcn_sched_barrier(0);          \
-      MMA_PASS(AC, BC, 0, 1);                     \
-      __builtin_amdgcn_sched_barrier(0);          \
-      LOAD_B(BP, (KB) + 1);                       \
-      __builtin_amdgcn_sched_barrier(0);          \
-      MMA_PASS(AC, BC, 1, 0);                     \
-      __builtin_amdgcn_sched_barrier(0);          \
-    } else {                                      \
-      LOAD_A(AP, (KB) + 2);                       \
-      LOAD_B(BP, (KB) + 1);                       \
-      __builtin_amdgcn_sched_barrier(0);          \
-      MMA3(AC, BC);                               \
-      __builtin_amdgcn_sched_barrier(0);          \
+  if constexpr (VAR & 128) {                      \
+    LOAD_B(BP, (KB) + 1);                         \
+    LOAD_A(AP, (KB) + PD);                        \
+    MMA3(AC, BC);                                 \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         \
+    }                                                            \
+    _Pragma("unroll") for (int g_ = 0; g_ < 4; ++g_) {           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         \
+    }                                                            \
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);           \
+    __builtin_amdgcn_sched_barrier(0);            \
+  } else if constexpr (VAR & 4) {                 \
+    LOAD_A(AP, (KB) + PD);                        \
+    LOAD_B(BP, (KB) + 1);                         \
+    __builtin_amdgcn_sched_barrier(0);            \
+    MMA3(AC, BC);                                 \
+    __builtin_amdgcn_sched_barrier(0);            \
+  } else {                                        \
+    LOAD_A(AP, (KB) + PD);                        \
+    LOAD_B(BP, (KB) + 1);                         \
+    MMA3(AC, BC);                                 \
+    _Pragma("unroll") for (int g_ = 0; g_ < 4; ++g_) {           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);         \
+    }                                                            \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {           \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);         \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);         \
+    }                                                            \
+    __builtin_amdgcn_sched_barrier(0);            \
+  }
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p) LOAD_A(A[p], p);
+    LOAD_B(B[0], 0);
+    for (int kb = 0; kb < KBLK; kb += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) STEP(kb + u, A[u % RS], A[(u + PD) % RS], B[u & 1], B[(u + 1) & 1]);
     }
-    LOAD_A(A0, 0);
-    LOAD_A(A1, 1);
-    LOAD_B(B0, 0);
-    for (int kb = 0; kb < KBLK; kb += 6) {
-      STEP(kb + 0, A0, A2, B0, B1);
-      STEP(kb + 1, A1, A0, B1, B0);
-      STEP(kb + 2, A2, A1, B0, B1);
-      STEP(kb + 3, A0, A2, B1, B0);
-      STEP(kb + 4, A1, A0, B0, B1);
-      STEP(kb + 5, A2, A1, B1, B0);
-    }
-#undef STEP
-#undef LOAD_B
-#undef LOAD_A
     stamp(st_k);
+    Wl += CONVX_U4_PER_LAYER;
     __syncthreads();   // every wave has finished reading this layer's input image
 
     // epilogue: y = ReLU(acc * 2^-e + bias) (conv B: acc already holds 2^e * x, the residual)
-    const bool conv_a = (L & 1) == 0;
-    epilogue(W.convx_inv[L], W.conv_b + L * 256, conv_a, conv_a ? 1.0f / W.convx_inv[L + 1] : 0.f);
+    if ((L & 1) == 0)
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1]);
+    else
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f);
     __syncthreads();
     stamp(st_epi);
   }
+#undef STEP
+#undef LOAD_B
+#undef LOAD_A
   if (overflow) atomicOr(D.pr.err, ERR_F16);
 
   // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
-  float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
-  float* fv = fp + XB * 64;                            // [XB][32]: vconv features (30) + clock
-  float* red = fv + XB * 32;                           // [XB][256]
-  for (int t = tid; t < XB * 90; t += 256) {
-    const int bb = t / 90, o = (t % 90) / 30, p = t % 30;
-    const float* wr = o < 2 ? W.pconv_w + o * 256 : W.vconv_w;
-    float s = 0.f;
-    for (int c = 0; c < 32; ++c) {
-      const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ioff(0, bb, p, c));
-      const f16x8 xl = *reinterpret_cast<const f16x8*>(smem + ioff(1, bb, p, c));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += wr[8 * c + j] * ((float)xh[j] + (float)xl[j]);
-    }
-    s = fmaxf(s + (o < 2 ? W.pconv_b[o] : W.vconv_b[0]), 0.f);
-    if (o < 2) fp[bb * 64 + o * 30 + p] = s; else fv[bb * 32 + p] = s;
-  }
-  if (tid < XB) {
-    const int b = b0 + tid;
-    const float clk = b < nb ? encode_clock(unpack(pos[b])) : 0.f;
-    fp[tid * 64 + 60] = clk;
-    fv[tid * 32 + 30] = clk;
-  }
-  __syncthreads();
-  {
-    const int j = tid;
-#pragma unroll
-    for (int bb = 0; bb < XB; ++bb) {
-      float hsum = W.vl1_b[j];
-      for (int i = 0; i < 31; ++i) hsum += W.vl1_w[j * 31 + i] * fv[bb * 32 + i];
-      red[bb * 256 + j] = W.vl2_w[j] * fmaxf(hsum, 0.f);
-    }
-  }
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s)
-#pragma unroll
-      for (int bb = 0; bb < XB; ++bb) red[bb * 256 + tid] += red[bb * 256 + tid + s];
-    __syncthreads();
-  }
+  heads_reduce(smem, pos, b0, nb, W, tid);
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
@@ -389,56 +265,7 @@ __global__ __launch_bounds__(256, 1) void k_net_x(Dev D, NetWeights W, const Pos
       stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;  // 100 MHz ticks
     }
   }
-  // wave bb finishes board bb: value, then policy logits / legal softmax
-  const int bb = wave;
-  const int b = b0 + bb;
-  if (b >= nb) return;
-  const float v = tanhf(red[bb * 256] + W.vl2_b[0]);
-  const float* f = fp + bb * 64;
-  if (mode == NET_FULL_LOGITS) {
-    if (lane == 0) values_out[b] = v;
-    for (int a = lane; a < NUM_ACTIONS; a += 64) {
-      float l = W.plin_b[a];
-      for (int j = 0; j < 61; ++j) l += W.plin_w[a * 61 + j] * f[j];
-      logits_out[(size_t)b * NUM_ACTIONS + a] = l;
-    }
-    return;
-  }
-  if (lane == 0) D.lf.v[b] = v;
-  const int t = D.lf.tree[b];
-  const uint32_t n = D.lf.node[b];
-  const int k = D.tr.node_k[(size_t)t * D.tr.NC + n];
-  const uint32_t e0 = D.tr.node_e0[(size_t)t * D.tr.NC + n];
-  const uint16_t* codes = D.tr.e_code + (size_t)t * D.tr.EC + e0;
-  float lg[KMAX / 64];
-  float mx = -__builtin_inff();
-#pragma unroll
-  for (int r = 0; r < KMAX / 64; ++r) {
-    const int c = lane + 64 * r;
-    float l = -__builtin_inff();
-    if (c < k) {
-      const int a = codes[c];
-      l = W.plin_b[a];
-      for (int j = 0; j < 61; ++j) l += W.plin_w[a * 61 + j] * f[j];
-    }
-    lg[r] = l;
-    mx = fmaxf(mx, l);
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  float sum = 0.f;
-#pragma unroll
-  for (int r = 0; r < KMAX / 64; ++r) {
-    lg[r] = (lane + 64 * r < k) ? expf(lg[r] - mx) : 0.f;
-    sum += lg[r];
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
-#pragma unroll
-  for (int r = 0; r < KMAX / 64; ++r) {
-    const int c = lane + 64 * r;
-    if (c < k) D.lf.P[(size_t)b * KMAX + c] = lg[r] / sum;
-  }
+  heads_out(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
 }
 
 template <bool S>
@@ -451,30 +278,32 @@ static void launch_variant(int var, dim3 grid, hipStream_t s, const Dev& d, cons
       hipLaunchKernelGGL((k_net_x<S, V>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, \
                          stamps);                                                                             \
       break;
-    MTAZ_VAR_CASE(1)
-    MTAZ_VAR_CASE(2)
-    MTAZ_VAR_CASE(8)
+    MTAZ_VAR_CASE(4)
+    MTAZ_VAR_CASE(128)
 #undef MTAZ_VAR_CASE
     default:
       hipLaunchKernelGGL((k_net_x<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   }
 }
 
-void launch_net_x(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
-                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
-                  int variant) {
+void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                      float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                      int variant) {
+  if (!(variant & NET_VAR_X))
+    return launch_net_y(d, w, pos, count, max_b, mode, logits_out, values_out, s, ev_begin, ev_end, variant);
   if (max_b <= 0) return;
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
-  launch_variant<false>(variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode, logits_out, values_out,
-                        nullptr);
+  launch_variant<false>(variant & ~NET_VAR_X, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode,
+                        logits_out, values_out, nullptr);
   if (ev_end) (void)hipEventRecord(ev_end, s);
 }
 
-void launch_net_x_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
-                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant) {
+void launch_net_f16x3_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                              float* values_out, unsigned long long* stamps, hipStream_t s, int variant) {
+  if (!(variant & NET_VAR_X)) return launch_net_y_stamped(d, w, pos, n, logits_out, values_out, stamps, s, variant);
   if (n <= 0) return;
-  launch_variant<true>(variant, dim3((n + XB - 1) / XB), s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS, logits_out,
-                       values_out, stamps);
+  launch_variant<true>(variant & ~NET_VAR_X, dim3((n + XB - 1) / XB), s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS,
+                       logits_out, values_out, stamps);
 }
 
 }  // namespace mtaz

@@ -1,0 +1,293 @@
+// k_net_y: the fused fp16x3 policy/value network (exp/policy.py:71-80 + the leaf priors of
+// exp/agent.py:67-69) on v_mfma_f32_16x16x32_f16.  Same algorithm, LDS image, residual
+// seeding and heads as k_net_x (mtaz_net.hip); only the MFMA shape and the fragment layouts
+// differ.  Under the chip's power limit the 16x16x32 shape holds a higher clock than 32x32x16
+// at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS item 7), and this kernel is MFMA-bound.
+//
+// Workgroup = 4 boards, 256 threads.  Wave w owns output channels [64w, 64w+64) as 4 channel
+// tiles of 16, times 4 boards x 2 square tiles of 16 (squares 0..15, 16..31; 30, 31 pad):
+// 32 accumulator tiles of 16x16 (128 AGPRs).  A conv's K = 2304 runs as 72 k-blocks of 32
+// contiguous k = tap*256 + ci, so a k-block is one tap and 32 input channels: lane l holds
+// A = W[co = 16ct + (l&15)][k = 32kb + 8(l>>4) + j] and B = X[k][square 16pt + (l&15)],
+// i.e. the 16-B chunk 4(kb&7) + (l>>4) of the source square's image row.
+#include <type_traits>
+
+#include "net_common.h"
+
+namespace mtaz {
+
+using namespace netc;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr int KBY = 72;   // k-blocks of 32 per conv
+
+// one split pass over the wave's 32 tiles: W part WP (0 hi / 1 lo) x X part XP.
+// SA[2*ct + part], SB[part*8 + t] with t = 2*board + square tile.
+#define YMMA(SA, SB, WP, XP)                                                                          \
+  {                                                                                                   \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < 4; ++ct_)                                               \
+    _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_)                                                  \
+      acc[ct_ * 8 + t_] = __builtin_amdgcn_mfma_f32_16x16x32_f16(SA[2 * ct_ + (WP)], SB[(XP) * 8 + t_], \
+                                                                 acc[ct_ * 8 + t_], 0, 0, 0);         \
+  }
+// Wh*Xh + Wh*Xl + Wl*Xh: 96 MFMAs, 31 independent ones between two updates of one accumulator
+#define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
+
+// VAR (in-process A/B, tools/bench_net.py): 0 = product schedule; 4, 16: see STEP
+template <bool STAMP, int VAR>
+__global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
+                                                  const int32_t* __restrict__ count, int max_b, int mode,
+                                                  float* __restrict__ logits_out, float* __restrict__ values_out,
+                                                  unsigned long long* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
+  const int nb = count ? *count : max_b;
+  const int b0 = blockIdx.x * XB;
+  if (b0 >= nb) return;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, n = lane & 15, g = lane >> 4;
+  unsigned long long t_prev = 0, st_stem = 0, st_k = 0, st_epi = 0, st_heads = 0;
+  unsigned long long t_start = 0, r_start = 0;
+  if constexpr (STAMP) {
+    t_prev = t_start = __builtin_amdgcn_s_memtime();
+    r_start = __builtin_amdgcn_s_memrealtime();
+  }
+  auto stamp = [&](unsigned long long& acc) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - t_prev;
+      t_prev = t;
+    }
+  };
+
+  // the lane's output squares: n (tile 0) and p1 = 16 + n (tile 1; 30, 31 are padding)
+  const int p1 = 16 + n;
+  const int ph0 = n / 5, pw0 = n % 5, ph1 = p1 / 5, pw1 = p1 % 5;
+  f32x4v acc[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) acc[i] = (f32x4v){0};
+  int overflow = 0;
+
+  // Epilogue (stem and every conv): y = ReLU(acc * 2^-e + bias) written in place as f16
+  // hi/lo; conv A seeds the accumulators with 2^e_next * x (conv B's residual), else resets.
+  // Lane l holds channels 16ct + 4(l>>4) + r of square 16pt + (l&15): 8 B per image part.
+  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next) {
+    constexpr bool conv_a = decltype(conv_a_t)::value;
+    float ymax = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int co0 = 64 * wave + 16 * ct + 4 * g;
+      const float4 bv = *reinterpret_cast<const float4*>(bias + co0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int bb = t >> 1, pt = t & 1;
+        f32x4v& a = acc[ct * 8 + t];
+        if (pt == 0 || p1 < 30) {
+          const int p = pt ? p1 : n;
+          const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1), al = ah + PARTB;
+          float y[4];
+          y[0] = fmaxf(__builtin_fmaf(a[0], inv, bv.x), 0.f);
+          y[1] = fmaxf(__builtin_fmaf(a[1], inv, bv.y), 0.f);
+          y[2] = fmaxf(__builtin_fmaf(a[2], inv, bv.z), 0.f);
+          y[3] = fmaxf(__builtin_fmaf(a[3], inv, bv.w), 0.f);
+          if constexpr (conv_a) {
+            const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
+            const f16x4 xl = *reinterpret_cast<const f16x4*>(smem + al);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf((float)xh[j], s_next, (float)xl[j] * s_next);
+          } else {
+            a = (f32x4v){0};
+          }
+          f16x4 yh, yl;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ymax = fmaxf(ymax, y[j]);
+            yh[j] = (_Float16)y[j];
+            yl[j] = (_Float16)__builtin_fmaf((float)yh[j], -1.f, y[j]);
+          }
+          *reinterpret_cast<f16x4*>(smem + ah) = yh;
+          *reinterpret_cast<f16x4*>(smem + al) = yl;
+        } else {
+          a = (f32x4v){0};
+        }
+      }
+    }
+    overflow |= ymax >= 65504.f;
+  };
+
+  // ---------------- stem: conv3x3 8->256, K = 3 k-blocks of (4 taps x 8 channels) ----------
+  char* simg = smem + IMGB;
+  stem_input(smem, simg, pos, b0, nb, W, tid);
+  __syncthreads();
+  {
+    const uint4* Ws = W.stemy + (size_t)(4 * wave) * 3 * 128 + lane;
+    for (int kb = 0; kb < 3; ++kb) {
+      f16x8 SA[8], SB[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        SA[2 * c] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128]);
+        SA[2 * c + 1] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128 + 64]);
+      }
+      const int tap = 4 * kb + g;
+      const int r0 = tap < 9 ? src_row(n, ph0, pw0, tap) : ZROW;
+      const int r1 = tap < 9 ? src_row(p1, ph1, pw1, tap) : ZROW;
+#pragma unroll
+      for (int part = 0; part < 2; ++part)
+#pragma unroll
+        for (int bb = 0; bb < XB; ++bb) {
+          SB[part * 8 + 2 * bb] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r0) * 16);
+          SB[part * 8 + 2 * bb + 1] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r1) * 16);
+        }
+      YMMA3(SA, SB);
+    }
+  }
+  epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f);
+  __syncthreads();
+  stamp(st_stem);
+
+  // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
+  // Weights stream from L2 through a 3-slot register ring two k-blocks ahead; activation
+  // fragments come from LDS one k-block ahead, hi parts first (the order pass 1 uses them).
+  constexpr int PD = 2, RS = 3, U = 6;
+  static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
+  f16x8 A[RS][8], B[2][16];
+  const uint4* Wl = W.convy + (size_t)(4 * wave) * KBY * 128 + lane;
+#define LOAD_A(S, KB)                                                                 \
+  {                                                                                   \
+    const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
+    const uint4* p_ = Wl + (size_t)kk_ * 128;                                         \
+    _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_) {                                \
+      S[2 * c_] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128]);                      \
+      S[2 * c_ + 1] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128 + 64]);             \
+    }                                                                                 \
+  }
+#define LOAD_BP(S, KB, PART)                                                          \
+  {                                                                                   \
+    const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
+    const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
+    const int r0_ = src_row(n, ph0, pw0, tap_), r1_ = src_row(p1, ph1, pw1, tap_);    \
+    const int o0_ = r0_ * RB + ((ch_ ^ (r0_ & 15)) << 4);                             \
+    const int o1_ = r1_ * RB + ((ch_ ^ (r1_ & 15)) << 4);                             \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
+      const char* base_ = smem + (PART) * PARTB + bb_ * IROWS * RB;                   \
+      S[(PART) * 8 + 2 * bb_] = *reinterpret_cast<const f16x8*>(base_ + o0_);        \
+      S[(PART) * 8 + 2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);    \
+    }                                                                                 \
+  }
+#define LOAD_B(S, KB) LOAD_BP(S, KB, 0) LOAD_BP(S, KB, 1)
+// Product schedule: the next k-block's 16 LDS reads one per 2 MFMAs at the top of the step,
+// then the 8 weight loads one per 4 MFMAs, then the remaining 32 MFMAs.  Variants: 4 = all
+// loads first, then the 96 MFMAs; 16 = the Wh*Xl pass first so the next Xl reuses its
+// registers.
+#define STEP(KB, AC, AP, BC, BP)                                   \
+  if constexpr (VAR & 4) {                                         \
+    LOAD_B(BP, (KB) + 1);                                          \
+    LOAD_A(AP, (KB) + PD);                                         \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    YMMA3(AC, BC);                                                 \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } else if constexpr (VAR & 16) {                                 \
+    /* Wh*Xl first: Xl(kb) dies after a third of the step and Xl(kb+1) reuses it */ \
+    YMMA(AC, BC, 0, 1);                                            \
+    LOAD_BP(BP, (KB) + 1, 0);                                      \
+    LOAD_A(AP, (KB) + PD);                                         \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           \
+    }                                                              \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);           \
+    }                                                              \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    YMMA(AC, BC, 0, 0);                                            \
+    LOAD_BP(BP, (KB) + 1, 1);                                      \
+    YMMA(AC, BC, 1, 0);                                            \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           \
+    }                                                              \
+    __builtin_amdgcn_sched_group_barrier(0x008, 48, 0);            \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } else {                                                         \
+    LOAD_B(BP, (KB) + 1);                                          \
+    LOAD_A(AP, (KB) + PD);                                         \
+    YMMA3(AC, BC);                                                 \
+    _Pragma("unroll") for (int g_ = 0; g_ < 16; ++g_) {            \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           \
+    }                                                              \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);           \
+    }                                                              \
+    __builtin_amdgcn_sched_group_barrier(0x008, 32, 0);            \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  }
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p) LOAD_A(A[p], p);
+    LOAD_B(B[0], 0);
+    for (int kb = 0; kb < KBY; kb += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) STEP(kb + u, A[u % RS], A[(u + PD) % RS], B[u & 1], B[(u + 1) & 1]);
+    }
+    stamp(st_k);
+    Wl += CONVX_U4_PER_LAYER;
+    __syncthreads();   // every wave has finished reading this layer's input image
+    if ((L & 1) == 0)
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1]);
+    else
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f);
+    __syncthreads();
+    stamp(st_epi);
+  }
+#undef STEP
+#undef LOAD_B
+#undef LOAD_A
+  if (overflow) atomicOr(D.pr.err, ERR_F16);
+
+  // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
+  heads_reduce(smem, pos, b0, nb, W, tid);
+  stamp(st_heads);
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      stamps[blockIdx.x * 6 + 0] = st_stem;
+      stamps[blockIdx.x * 6 + 1] = st_k;
+      stamps[blockIdx.x * 6 + 2] = st_epi;
+      stamps[blockIdx.x * 6 + 3] = st_heads;
+      stamps[blockIdx.x * 6 + 4] = __builtin_amdgcn_s_memtime() - t_start;
+      stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
+    }
+  }
+  heads_out(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
+}
+
+template <bool S>
+static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
+                     const int32_t* count, int max_b, int mode, float* logits, float* values,
+                     unsigned long long* stamps) {
+  if (var & 4)
+    hipLaunchKernelGGL((k_net_y<S, 4>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 16)
+    hipLaunchKernelGGL((k_net_y<S, 16>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else
+    hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+}
+
+void launch_net_y(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                  int variant) {
+  if (max_b <= 0) return;
+  if (ev_begin) (void)hipEventRecord(ev_begin, s);
+  launch_y<false>(variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode, logits_out, values_out,
+                  nullptr);
+  if (ev_end) (void)hipEventRecord(ev_end, s);
+}
+
+void launch_net_y_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant) {
+  if (n <= 0) return;
+  launch_y<true>(variant, dim3((n + XB - 1) / XB), s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS, logits_out,
+                 values_out, stamps);
+}
+
+}  // namespace mtaz

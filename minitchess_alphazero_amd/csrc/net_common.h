@@ -1,0 +1,177 @@
+// Pieces shared by the fused fp16x3 network kernels (k_net_x: v_mfma_f32_32x32x16_f16,
+// mtaz_net.hip; k_net_y: v_mfma_f32_16x16x32_f16, mtaz_net16.hip): the LDS activation image,
+// the stem input, and the policy/value heads (exp/policy.py:62-80, exp/agent.py:67-69).
+#pragma once
+#include "engine.h"
+
+namespace mtaz {
+namespace netc {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int XB = 4;                     // boards per workgroup
+constexpr int IROWS = 31;                 // image rows: squares 0..29 + zero row
+constexpr int ZROW = 30;
+constexpr int RB = 512;                   // bytes per row: 256 channels x f16
+constexpr int PARTB = XB * IROWS * RB;    // 63,488 B per part (hi / lo)
+constexpr int IMGB = 2 * PARTB;           // 126,976 B
+constexpr int AUXB = XB * 8 * 56 * 4;     // 7,168 B: stem input / head features
+
+// byte offset of 16-B channel chunk `chunk` (8 channels) of image row `row`; the chunk index
+// is XOR-swizzled with the row so that a wave's 16-B reads of one chunk over consecutive rows
+// land in distinct bank groups
+__device__ __forceinline__ int ioff(int part, int bb, int row, int chunk) {
+  return part * PARTB + (bb * IROWS + row) * RB + ((chunk ^ (row & 15)) << 4);
+}
+
+// image row holding the source square of output square `p` (row ph, file pw) for tap
+// (dh, dw) = (tap/3 - 1, tap%3 - 1), or the zero row (off-board / padding square)
+__device__ __forceinline__ int src_row(int p, int ph, int pw, int tap) {
+  const int dh = tap / 3 - 1, dw = tap - 3 * (tap / 3) - 1;
+  const int r = ph + dh, c = pw + dw;
+  return (p < 30 && r >= 0 && r < 6 && c >= 0 && c < 5) ? p + 5 * dh + dw : ZROW;
+}
+
+// Zero the image's zero rows and build the stem input image in `simg` (aux region):
+// [part][board][row 31][8 ch f16], channel c = plane*4 + e of Embedding(7,4) applied to the
+// own / opponent token planes (exp/policy.py:71-74, encoder exp/environment.py:63-75).
+// Caller: __syncthreads() before reading.
+__device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* pos, int b0, int nb,
+                                           const NetWeights& W, int tid) {
+  for (int i = tid; i < 2 * XB * 32; i += 256) {
+    const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
+    *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < 2 * XB * IROWS; i += 256) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if (tid < XB * 30) {
+    const int bb = tid / 30, i = tid % 30;          // i = square index in the mover's view
+    const int b = b0 + bb;
+    int own = 0, opp = 0;
+    if (b < nb) {
+      const BB bd = unpack(pos[b]);
+      const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
+      const int t = piece_type_at(bd, s);
+      const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
+      own = mine ? token_code(t) : 0;
+      opp = (t && !mine) ? token_code(t) : 0;
+    }
+    f16x8 xh, xl;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float v = W.emb[(c < 4 ? own : opp) * 4 + (c & 3)];
+      xh[c] = (_Float16)v;
+      xl[c] = (_Float16)(v - (float)xh[c]);
+    }
+    *reinterpret_cast<f16x8*>(simg + (bb * IROWS + i) * 16) = xh;
+    *reinterpret_cast<f16x8*>(simg + ((XB + bb) * IROWS + i) * 16) = xl;
+  }
+}
+
+// Heads, part 1 (all 256 threads): policy conv 256->2 and value conv 256->1 (1x1, BN folded,
+// ReLU) from the final image, the clock feature, the value MLP hidden layer and its
+// reduction.  Leaves fp [XB][64] (60 policy features + clock), red[bb*256] = value pre-tanh.
+__device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0, int nb, const NetWeights& W,
+                                             int tid) {
+  float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
+  float* fv = fp + XB * 64;                            // [XB][32]: vconv features (30) + clock
+  float* red = fv + XB * 32;                           // [XB][256]
+  for (int t = tid; t < XB * 90; t += 256) {
+    const int bb = t / 90, o = (t % 90) / 30, p = t % 30;
+    const float* wr = o < 2 ? W.pconv_w + o * 256 : W.vconv_w;
+    float s = 0.f;
+    for (int c = 0; c < 32; ++c) {
+      const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ioff(0, bb, p, c));
+      const f16x8 xl = *reinterpret_cast<const f16x8*>(smem + ioff(1, bb, p, c));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += wr[8 * c + j] * ((float)xh[j] + (float)xl[j]);
+    }
+    s = fmaxf(s + (o < 2 ? W.pconv_b[o] : W.vconv_b[0]), 0.f);
+    if (o < 2) fp[bb * 64 + o * 30 + p] = s; else fv[bb * 32 + p] = s;
+  }
+  if (tid < XB) {
+    const int b = b0 + tid;
+    const float clk = b < nb ? encode_clock(unpack(pos[b])) : 0.f;
+    fp[tid * 64 + 60] = clk;
+    fv[tid * 32 + 30] = clk;
+  }
+  __syncthreads();
+  {
+    const int j = tid;
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) {
+      float hsum = W.vl1_b[j];
+      for (int i = 0; i < 31; ++i) hsum += W.vl1_w[j * 31 + i] * fv[bb * 32 + i];
+      red[bb * 256 + j] = W.vl2_w[j] * fmaxf(hsum, 0.f);
+    }
+  }
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s)
+#pragma unroll
+      for (int bb = 0; bb < XB; ++bb) red[bb * 256 + tid] += red[bb * 256 + tid + s];
+    __syncthreads();
+  }
+}
+
+// Heads, part 2 (wave bb finishes board bb): value = tanh, then either the full 554 logits
+// (evaluate mode) or the leaf priors = softmax over the legal moves' logits in the node's
+// legal-list order (exp/agent.py:67-69), written to D.lf.
+__device__ __forceinline__ void heads_out(const Dev& D, char* smem, int b0, int nb, const NetWeights& W, int mode,
+                                          float* logits_out, float* values_out, int wave, int lane) {
+  const float* fp = reinterpret_cast<const float*>(smem + IMGB);
+  const float* red = fp + XB * 64 + XB * 32;
+  const int bb = wave;
+  const int b = b0 + bb;
+  if (b >= nb) return;
+  const float v = tanhf(red[bb * 256] + W.vl2_b[0]);
+  const float* f = fp + bb * 64;
+  if (mode == NET_FULL_LOGITS) {
+    if (lane == 0) values_out[b] = v;
+    for (int a = lane; a < NUM_ACTIONS; a += 64) {
+      float l = W.plin_b[a];
+      for (int j = 0; j < 61; ++j) l += W.plin_w[a * 61 + j] * f[j];
+      logits_out[(size_t)b * NUM_ACTIONS + a] = l;
+    }
+    return;
+  }
+  if (lane == 0) D.lf.v[b] = v;
+  const int t = D.lf.tree[b];
+  const uint32_t n = D.lf.node[b];
+  const int k = D.tr.node_k[(size_t)t * D.tr.NC + n];
+  const uint32_t e0 = D.tr.node_e0[(size_t)t * D.tr.NC + n];
+  const uint16_t* codes = D.tr.e_code + (size_t)t * D.tr.EC + e0;
+  float lg[KMAX / 64];
+  float mx = -__builtin_inff();
+#pragma unroll
+  for (int r = 0; r < KMAX / 64; ++r) {
+    const int c = lane + 64 * r;
+    float l = -__builtin_inff();
+    if (c < k) {
+      const int a = codes[c];
+      l = W.plin_b[a];
+      for (int j = 0; j < 61; ++j) l += W.plin_w[a * 61 + j] * f[j];
+    }
+    lg[r] = l;
+    mx = fmaxf(mx, l);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < KMAX / 64; ++r) {
+    lg[r] = (lane + 64 * r < k) ? expf(lg[r] - mx) : 0.f;
+    sum += lg[r];
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+#pragma unroll
+  for (int r = 0; r < KMAX / 64; ++r) {
+    const int c = lane + 64 * r;
+    if (c < k) D.lf.P[(size_t)b * KMAX + c] = lg[r] / sum;
+  }
+}
+
+}  // namespace netc
+}  // namespace mtaz

@@ -25,6 +25,7 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision']
 
+NET_VAR_X = 512   # mtaz_set_net_variant bit: k_net_x (v_mfma_f32_32x32x16_f16) instead of k_net_y
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
 # one trunk conv on one board: 30 positions x 256 out x 2304 K, 2 FLOP/MAC
@@ -88,6 +89,12 @@ class Engine:
     def set_precision(self, precision):
         """'f16x3' (default: fp16 hi/lo split MFMA, fp32-accurate) or 'fp32' (fp32 MFMA)."""
         _lib.check(self.L.mtaz_set_precision(self.h, {'fp32': 0, 'f16x3': 1}[precision]))
+
+    def set_net_variant(self, variant):
+        """Select the fp16x3 network kernel code variant: 0 = product k_net_y
+        (v_mfma_f32_16x16x32_f16); NET_VAR_X (512) routes to k_net_x (32x32x16); the low
+        bits pick A/B schedules of either kernel."""
+        _lib.check(self.L.mtaz_set_net_variant(self.h, int(variant)))
 
     def set_seed_base(self, seed_base):
         """Game slot g of the next play() uses np.random.seed(seed_base + g) semantics."""

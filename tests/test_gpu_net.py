@@ -23,13 +23,21 @@ def _softmax(x):
     return e / e.sum()
 
 
-@pytest.fixture(scope='module', params=['f16x3', 'fp32'])
+# f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 16);
+# f16x3-x* = k_net_x (32x32x16 MFMA, variant bit 512) and its schedules; fp32 = fp32 MFMA path
+NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4),
+               'f16x3-y16': ('f16x3', 16), 'f16x3-x': ('f16x3', 512), 'f16x3-x128': ('f16x3', 512 + 128)}
+
+
+@pytest.fixture(scope='module', params=list(NET_KERNELS))
 def engine(request):
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.network import Network
     import torch
     eng = Engine(n_games=64, sims=8)
-    eng.set_precision(request.param)
+    prec, var = NET_KERNELS[request.param]
+    eng.set_precision(prec)
+    eng.set_net_variant(var)
     torch.manual_seed(0)
     net = Network()
     eng.set_weights(net)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Network-only microbenchmark and in-process A/B of k_net_x code variants.
+"""Network-only microbenchmark and in-process A/B of the fp16x3 network kernels
+(variant 0 = product k_net_y; +512 = k_net_x; low bits = schedules).
 
 For each variant (interleaved over --rounds, one process, one device; MI355X devices
 clock ~10% apart, so only same-process comparisons mean anything):

@@ -1,0 +1,19 @@
+#!/bin/bash
+# HBM traffic of the dominant kernel (k_net_y, product; k_net_x when selected) from PMC counters, one counter group per
+# rocprofv3 pass (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950), counters
+# restricted to the k_net_* kernels.  No trace domains are combined with --pmc.
+# Summaries: python tools/pmc_summary.py gpurun_out/pmc -> profiles/conv_traffic.json
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/pmc
+ARGS="${BENCH_ARGS:---no-cpu-baseline}"
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i + 1))
+  timeout -k 10 ${PMC_TIMEOUT:-420} rocprofv3 --pmc $grp --kernel-include-regex "k_net_[xy]" \
+    -d gpurun_out/pmc/p$i -o pmc --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/p$i.log 2>&1
+  rc=$?
+  echo "pmc pass $i ($grp) rc=$rc"
+  tail -2 gpurun_out/pmc/p$i.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
