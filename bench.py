@@ -23,6 +23,8 @@ sys.path.insert(0, HERE)
 METRIC = 'self-play games/sec + MCTS sims/sec at 1/2/4/8 MI355X (fixed sims/move)'
 FP32_MATRIX_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md chip table (f32-input MFMA = f32 vector rate)
 F16_MATRIX_PEAK_TFLOPS = 2500.0      # dense f16/bf16 MFMA (MI355X_MICROARCH.md; sparsity figures excluded)
+HBM_PEAK_GBS = 8000.0                # MI355X_MICROARCH.md HBM peak
+TREE_BYTES_PER_SIM = 700             # SURVEY 8d algorithmic bytes per simulation of the tree walk
 
 
 def cpu_baseline(sims, threads, seconds_cap):
@@ -95,7 +97,7 @@ def main():
             dist.barrier()
 
     tot = {'sims': 0.0, 'nn_evals': 0.0, 'plies': 0.0, 'trunk_ms': 0.0, 'trunk_boards': 0.0, 'waves': 0.0,
-           'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0}
+           'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0, 'select_ms': 0.0}
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -163,6 +165,17 @@ def main():
                      'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
                      'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch,
                      'mfma_passes': 3 if f16x3 else 1},
+        # secondary roofline: the tree kernel k_select, HBM/latency-bound; algorithmic
+        # bytes per simulation = SURVEY's estimate (path nodes: header + k edge reads + edge update,
+        # leaf insert, hash probe, NN input) at k ~ 7.5, depth ~ 2
+        'roofline_tree': {'bound': 'hbm', 'kernel': 'k_select', 'bytes_per_sim': TREE_BYTES_PER_SIM,
+                          'achieved': tot['sims'] * TREE_BYTES_PER_SIM / (tot['select_ms'] * 1e-3) / 1e9
+                          if tot['select_ms'] > 0 else None,
+                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                          'frac': tot['sims'] * TREE_BYTES_PER_SIM / (tot['select_ms'] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                          if tot['select_ms'] > 0 else None,
+                          'avg_launch_ms': tot['select_ms'] / tot['waves'] if tot['waves'] else None,
+                          'share_of_wall': tot['select_ms'] / 1e3 / dt},
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
     }

@@ -427,7 +427,7 @@ struct PlyRec {
 
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
-  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_COUNT
+  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS, ST_COUNT
 };
 
 template <class F>
@@ -1012,18 +1012,20 @@ extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t
 
 static int sim_gpu(mtaz_engine* h, int sim) {
   HIPCHK(hipMemsetAsync(h->d.lf.count, 0, 4, h->stream));
-  launch_select(h->d, sim, h->stream);
+  // timing: per wave three events on the engine stream: [select begin, network begin, network end]
   hipEvent_t eb = nullptr, ee = nullptr;
   if (h->timing) {
-    const size_t need = 2 * (size_t)(h->wave + 1);
+    const size_t need = 3 * (size_t)(h->wave + 1);
     while (h->ev.size() < need) {
       hipEvent_t e;
       HIPCHK(hipEventCreate(&e));
       h->ev.push_back(e);
     }
-    eb = h->ev[2 * h->wave];
-    ee = h->ev[2 * h->wave + 1];
+    HIPCHK(hipEventRecord(h->ev[3 * h->wave], h->stream));
+    eb = h->ev[3 * h->wave + 1];
+    ee = h->ev[3 * h->wave + 2];
   }
+  launch_select(h->d, sim, h->stream);
   launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, eb, ee);
   launch_backup(h->d, h->stream);
   if (h->wave < h->count_log_cap)
@@ -1245,12 +1247,14 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     HIPCHK(hipMemcpy(counts.data(), h->d_count_log, counts.size() * 4, hipMemcpyDeviceToHost));
   double evals = 0;
   for (int c : counts) evals += c;
-  double trunk_ms = 0, trunk_boards = 0;
+  double trunk_ms = 0, trunk_boards = 0, select_ms = 0;
   if (h->timing) {
     for (int wv = 0; wv < h->wave && wv < (int)counts.size(); ++wv) {
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, h->ev[2 * wv], h->ev[2 * wv + 1]));
+      float ms = 0, sms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, h->ev[3 * wv + 1], h->ev[3 * wv + 2]));
+      HIPCHK(hipEventElapsedTime(&sms, h->ev[3 * wv], h->ev[3 * wv + 1]));
       trunk_ms += ms;
+      select_ms += sms;
       trunk_boards += counts[wv];
     }
   }
@@ -1279,6 +1283,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_MAX_NODES] = mxn;
   h->stats[ST_SYNC_MS] = sync_ms;
   h->stats[ST_NET_PREC] = h->precision;
+  h->stats[ST_SELECT_MS] = select_ms;
   return 0;
 }
 

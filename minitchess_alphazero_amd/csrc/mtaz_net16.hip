@@ -32,7 +32,8 @@ constexpr int KBY = 72;   // k-blocks of 32 per conv
 // Wh*Xh + Wh*Xl + Wl*Xh: 96 MFMAs, 31 independent ones between two updates of one accumulator
 #define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
 
-// VAR (in-process A/B, tools/bench_net.py): 0 = product schedule; 4, 16: see STEP
+// VAR (in-process A/B, tools/bench_net.py): 0 = product schedule; 4, 16, 32, 64, 128: see the
+// trunk.  In-process A/B on one MI355X (4096 boards): 0 5.01 ms, 64 5.04, 128 5.06, 4 5.25-5.34.
 template <bool STAMP, int VAR>
 __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
@@ -144,11 +145,16 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   stamp(st_stem);
 
   // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
-  // Weights stream from L2 through a 3-slot register ring two k-blocks ahead; activation
-  // fragments come from LDS one k-block ahead, hi parts first (the order pass 1 uses them).
-  constexpr int PD = 2, RS = 3, U = 6;
+  // Weights stream from L2 through a 3-slot register ring two k-blocks ahead; the next
+  // k-block's 16 activation fragments are read from LDS during the current step (product
+  // schedule, STEP below).  Variants 128 / 64 run each step as two half-steps, one per square
+  // tile, so only 8 activation fragments are live (a 2 x 8-fragment ring): 128 with
+  // sched_group_barrier, 64 with the order pinned by sched_barrier (no accumulator copies).
+  // variant 32: weights one k-block ahead (2-slot ring, unroll 2) for lower register pressure
+  constexpr bool HALVES = (VAR & (64 | 128)) != 0;
+  constexpr int PD = (VAR & 32) ? 1 : 2, RS = PD + 1, U = (VAR & 32) ? 2 : 6;
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
-  f16x8 A[RS][8], B[2][16];
+  f16x8 A[RS][8], B[2][16], BH[2][8];
   const uint4* Wl = W.convy + (size_t)(4 * wave) * KBY * 128 + lane;
 #define LOAD_A(S, KB)                                                                 \
   {                                                                                   \
@@ -173,8 +179,85 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     }                                                                                 \
   }
 #define LOAD_B(S, KB) LOAD_BP(S, KB, 0) LOAD_BP(S, KB, 1)
-// Product schedule: the next k-block's 16 LDS reads one per 2 MFMAs at the top of the step,
-// then the 8 weight loads one per 4 MFMAs, then the remaining 32 MFMAs.  Variants: 4 = all
+// one square tile's fragments of k-block KB: S[part*4 + board]
+#define LOAD_BH(S, KB, PT)                                                            \
+  {                                                                                   \
+    const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
+    const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
+    const int r_ = (PT) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);   \
+    const int o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                \
+    _Pragma("unroll") for (int part_ = 0; part_ < 2; ++part_)                         \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                              \
+      S[part_ * 4 + bb_] = *reinterpret_cast<const f16x8*>(smem + part_ * PARTB + bb_ * IROWS * RB + o_); \
+  }
+// weight fragments of channel tiles C0, C0+1 of k-block KB
+#define LOAD_AH(S, KB, C0)                                                            \
+  {                                                                                   \
+    const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
+    const uint4* p_ = Wl + (size_t)kk_ * 128;                                         \
+    _Pragma("unroll") for (int c_ = (C0); c_ < (C0) + 2; ++c_) {                      \
+      S[2 * c_] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128]);                      \
+      S[2 * c_ + 1] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128 + 64]);             \
+    }                                                                                 \
+  }
+#define YMMA_H(SA, SB, PT, WP, XP)                                                                    \
+  {                                                                                                   \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < 4; ++ct_)                                               \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
+      acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(                         \
+          SA[2 * ct_ + (WP)], SB[(XP) * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0);             \
+  }
+// variant 64: the same half-step in 12 chunks of 4 MFMAs in fixed program order
+// (sched_barrier between chunks), LDS reads 2 per chunk in chunks 0-3, weight loads 1 per
+// chunk in chunks 4-7
+#define HALF_PINNED(KB, PT, AC, AP, BC, BN, KBN, PTN)                                 \
+  {                                                                                   \
+    const int kk_ = (KBN) < KBY ? (KBN) : KBY - 1;                                    \
+    const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
+    const int r_ = (PTN) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);  \
+    const int o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                \
+    const int ka_ = ((KB) + PD) < KBY ? ((KB) + PD) : KBY - 1;                        \
+    const uint4* pa_ = Wl + (size_t)ka_ * 128;                                        \
+    _Pragma("unroll") for (int i_ = 0; i_ < 48; ++i_) {                               \
+      if (i_ % 4 == 0) {                                                              \
+        const int c_ = i_ / 4;                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                            \
+        if (c_ < 4) {                                                                 \
+          _Pragma("unroll") for (int q_ = 2 * c_; q_ < 2 * c_ + 2; ++q_)              \
+            BN[q_] = *reinterpret_cast<const f16x8*>(smem + (q_ >> 2) * PARTB + (q_ & 3) * IROWS * RB + o_); \
+        } else if (c_ < 8) {                                                          \
+          const int q_ = c_ - 4, ct_ = 2 * (PT) + (q_ >> 1), pp_ = q_ & 1;            \
+          AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
+        }                                                                             \
+        __builtin_amdgcn_sched_barrier(0);                                            \
+      }                                                                               \
+      const int ps_ = i_ >> 4, ct_ = (i_ >> 2) & 3, bb_ = i_ & 3;                     \
+      const int wp_ = ps_ == 2 ? 1 : 0, xp_ = ps_ == 1 ? 1 : 0;                       \
+      acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(         \
+          AC[2 * ct_ + wp_], BC[xp_ * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0); \
+    }                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  }
+// half-step: 48 MFMAs of square tile PT; meanwhile the next half's 8 LDS reads (one per 2
+// MFMAs) and half of the weight k-block KB+PD (one load per 4 MFMAs)
+#define HALF(KB, PT, AC, AP, BC, BN, KBN, PTN)                     \
+  {                                                                \
+    LOAD_BH(BN, KBN, PTN);                                         \
+    LOAD_AH(AP, (KB) + PD, 2 * (PT));                              \
+    YMMA_H(AC, BC, PT, 0, 0) YMMA_H(AC, BC, PT, 0, 1) YMMA_H(AC, BC, PT, 1, 0) \
+    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           \
+    }                                                              \
+    _Pragma("unroll") for (int g_ = 0; g_ < 4; ++g_) {             \
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);           \
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);           \
+    }                                                              \
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);            \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  }
+// Whole-k-block steps.  Product: the next k-block's 16 LDS reads one per 2 MFMAs at the top
+// of the step, then the 8 weight loads one per 4 MFMAs, then 32 MFMAs.  Variants: 4 = all
 // loads first, then the 96 MFMAs; 16 = the Wh*Xl pass first so the next Xl reuses its
 // registers.
 #define STEP(KB, AC, AP, BC, BP)                                   \
@@ -207,7 +290,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     }                                                              \
     __builtin_amdgcn_sched_group_barrier(0x008, 48, 0);            \
     __builtin_amdgcn_sched_barrier(0);                             \
-  } else {                                                         \
+  } else {   /* product, VAR 32 */                                  \
     LOAD_B(BP, (KB) + 1);                                          \
     LOAD_A(AP, (KB) + PD);                                         \
     YMMA3(AC, BC);                                                 \
@@ -225,10 +308,26 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   for (int L = 0; L < CONV_LAYERS; ++L) {
 #pragma unroll
     for (int p = 0; p < PD; ++p) LOAD_A(A[p], p);
-    LOAD_B(B[0], 0);
-    for (int kb = 0; kb < KBY; kb += U) {
+    if constexpr (HALVES) {
+      LOAD_BH(BH[0], 0, 0);
+      for (int kb = 0; kb < KBY; kb += U) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) STEP(kb + u, A[u % RS], A[(u + PD) % RS], B[u & 1], B[(u + 1) & 1]);
+        for (int u = 0; u < U; ++u) {
+          if constexpr (VAR & 64) {
+            HALF_PINNED(kb + u, 0, A[u % RS], A[(u + PD) % RS], BH[0], BH[1], kb + u, 1);
+            HALF_PINNED(kb + u, 1, A[u % RS], A[(u + PD) % RS], BH[1], BH[0], kb + u + 1, 0);
+          } else {
+            HALF(kb + u, 0, A[u % RS], A[(u + PD) % RS], BH[0], BH[1], kb + u, 1);
+            HALF(kb + u, 1, A[u % RS], A[(u + PD) % RS], BH[1], BH[0], kb + u + 1, 0);
+          }
+        }
+      }
+    } else {
+      LOAD_B(B[0], 0);
+      for (int kb = 0; kb < KBY; kb += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) STEP(kb + u, A[u % RS], A[(u + PD) % RS], B[u & 1], B[(u + 1) & 1]);
+      }
     }
     stamp(st_k);
     Wl += CONVX_U4_PER_LAYER;
@@ -241,7 +340,13 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     stamp(st_epi);
   }
 #undef STEP
+#undef HALF
+#undef HALF_PINNED
+#undef YMMA_H
+#undef LOAD_AH
+#undef LOAD_BH
 #undef LOAD_B
+#undef LOAD_BP
 #undef LOAD_A
   if (overflow) atomicOr(D.pr.err, ERR_F16);
 
@@ -265,7 +370,13 @@ template <bool S>
 static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
-  if (var & 4)
+  if (var & 64)
+    hipLaunchKernelGGL((k_net_y<S, 64>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 128)
+    hipLaunchKernelGGL((k_net_y<S, 128>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 32)
+    hipLaunchKernelGGL((k_net_y<S, 32>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 4)
     hipLaunchKernelGGL((k_net_y<S, 4>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 16)
     hipLaunchKernelGGL((k_net_y<S, 16>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);

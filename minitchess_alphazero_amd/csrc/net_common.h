@@ -33,6 +33,19 @@ __device__ __forceinline__ int src_row(int p, int ph, int pw, int tap) {
   return (p < 30 && r >= 0 && r < 6 && c >= 0 && c < 5) ? p + 5 * dh + dw : ZROW;
 }
 
+// piece nibble of square s (rules.h Pos layout) without a dynamically indexed local array
+__device__ __forceinline__ int nib_at(const Pos& p, int s) {
+  const int w = s >> 3;
+  const uint32_t word = w == 0 ? p.sq[0] : w == 1 ? p.sq[1] : w == 2 ? p.sq[2] : p.sq[3];
+  return (word >> (4 * (s & 7))) & 15;
+}
+
+// encode_clock (rules.h) straight from the packed info word
+__device__ __forceinline__ float clock_of(const Pos& p) {
+  const double c = (double)(p.info >> 16) + ((p.info & 1u) ? 0.0 : 0.5);
+  return (float)(c / 30.0);
+}
+
 // Zero the image's zero rows and build the stem input image in `simg` (aux region):
 // [part][board][row 31][8 ch f16], channel c = plane*4 + e of Embedding(7,4) applied to the
 // own / opponent token planes (exp/policy.py:71-74, encoder exp/environment.py:63-75).
@@ -50,10 +63,12 @@ __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* po
     const int b = b0 + bb;
     int own = 0, opp = 0;
     if (b < nb) {
-      const BB bd = unpack(pos[b]);
-      const int s = bd.white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
-      const int t = piece_type_at(bd, s);
-      const bool mine = ((bd.white ? bd.w : bd.b) >> s) & 1u;
+      const Pos pp = pos[b];
+      const bool white = pp.info & 1u;
+      const int s = white ? (5 - i / 5) * 5 + i % 5 : (i / 5) * 5 + (4 - i % 5);
+      const int nib = nib_at(pp, s);
+      const int t = nib & 7;
+      const bool mine = t && (((nib & 8) == 0) == white);
       own = mine ? token_code(t) : 0;
       opp = (t && !mine) ? token_code(t) : 0;
     }
@@ -92,7 +107,7 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
   }
   if (tid < XB) {
     const int b = b0 + tid;
-    const float clk = b < nb ? encode_clock(unpack(pos[b])) : 0.f;
+    const float clk = b < nb ? clock_of(pos[b]) : 0.f;
     fp[tid * 64 + 60] = clk;
     fv[tid * 32 + 30] = clk;
   }

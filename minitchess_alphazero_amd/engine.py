@@ -23,7 +23,8 @@ from . import _lib
 from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_to_fen
 
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
-              'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision']
+              'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
+              'select_ms']
 
 NET_VAR_X = 512   # mtaz_set_net_variant bit: k_net_x (v_mfma_f32_32x32x16_f16) instead of k_net_y
 # algorithmic work of one leaf evaluation: 319,122,946 MAC

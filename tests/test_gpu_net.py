@@ -23,10 +23,10 @@ def _softmax(x):
     return e / e.sum()
 
 
-# f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 16);
+# f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 64, 128);
 # f16x3-x* = k_net_x (32x32x16 MFMA, variant bit 512) and its schedules; fp32 = fp32 MFMA path
-NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4),
-               'f16x3-y16': ('f16x3', 16), 'f16x3-x': ('f16x3', 512), 'f16x3-x128': ('f16x3', 512 + 128)}
+NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4), 'f16x3-y128': ('f16x3', 128),
+               'f16x3-y64': ('f16x3', 64), 'f16x3-x': ('f16x3', 512)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
