@@ -53,6 +53,7 @@ def main():
     ap.add_argument('--games', type=int, default=4096, help='parallel games per GPU (BASELINE config 2: 4096)')
     ap.add_argument('--sims', type=int, default=64, help='MCTS simulations per move (config 2: 64)')
     ap.add_argument('--precision', default='f16x3', choices=['f16x3', 'fp32'])
+    ap.add_argument('--groups', type=int, default=1, help='game groups on separate HIP streams (mtaz_set_pipeline)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
@@ -87,6 +88,7 @@ def main():
     eng.set_weights(Network())
     eng.set_precision(args.precision)
     eng.set_timing(True)
+    eng.set_pipeline(args.groups)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
     for _ in range(args.warmup):
         eng.play()

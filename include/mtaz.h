@@ -119,8 +119,13 @@ int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
  * cycles, total 100 MHz ticks] from a separate diagnostic build (tools/bench_net.py) */
 int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int stamped, float* ms_out,
                   uint64_t* stamps_out);
-/* select a k_net_x code variant for A/B timing (0 = the product kernel) */
+/* select a network kernel code variant for A/B timing (0 = the product kernel k_net_y) */
 int mtaz_set_net_variant(mtaz_engine* h, int variant);
+/* mtaz_play over `groups` independent game groups (1 = off; must divide n_games): each group
+ * has its own HIP stream and host thread, so one group's tree kernels and network tail run
+ * while another's network occupies the GPU.  Games keep their global seeds, so results are
+ * identical for any group count.  Applies to full-batch mtaz_play(h, n_games, 0) only. */
+int mtaz_set_pipeline(mtaz_engine* h, int groups);
 
 /* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */

@@ -491,8 +491,11 @@ struct mtaz_engine {
   bool timing = false;
   std::vector<hipEvent_t> ev;
   int wave = 0;
+  int groups = 1;                       // mtaz_set_pipeline
+  std::vector<mtaz_engine*> parts;      // per-group engines (borrow this engine's weights)
 
   ~mtaz_engine() {
+    for (mtaz_engine* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     for (auto e : ev) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
@@ -911,6 +914,16 @@ extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   return 0;
 }
 
+extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
+  if (groups < 1 || h->G % groups != 0) return set_err(MTAZ_E_FAIL, "groups=%d must divide n_games=%d", groups, h->G);
+  if (groups != h->groups) {
+    for (mtaz_engine* p : h->parts) delete p;
+    h->parts.clear();
+  }
+  h->groups = groups;
+  return 0;
+}
+
 extern "C" int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base) {
   h->seed_base = seed_base;
   return 0;
@@ -1139,9 +1152,64 @@ extern "C" int mtaz_set_timing(mtaz_engine* h, int on) {
 // -> `sims` GPU waves of select / network / backup with no host sync -> root visit
 // counts -> host action choice (choice with p while fullmove < tau, else argmax with a
 // random tie-break, exp/agent.py:110-119) -> apply on device.
+// Full-batch self-play over h->groups game groups, one sub-engine (own stream, trees, leaf
+// batch) and one host thread per group.  Sub-engine i plays global games
+// [i*G/groups, (i+1)*G/groups) with seed_base + i*G/groups; records and counters are merged
+// back in game order, so the result equals the single-group run.
+static int play_groups(mtaz_engine* h) {
+  const int ng = h->groups, Gp = h->G / ng;
+  if (h->parts.empty()) {
+    for (int i = 0; i < ng; ++i) {
+      mtaz_engine* p = mtaz_create(h->device, Gp, h->sims, h->cpuct, h->tau, h->alpha, h->eps, 0, h->cast_mode,
+                                   h->flags, h->move_cap);
+      if (!p) return MTAZ_E_DEVICE;
+      h->parts.push_back(p);
+    }
+  }
+  for (int i = 0; i < ng; ++i) {
+    mtaz_engine* p = h->parts[i];
+    p->w = h->w;                 // borrowed device weights (owned by h)
+    p->weights_ok = true;
+    p->precision = h->precision;
+    p->variant = h->variant;
+    p->timing = h->timing;
+    p->seed_base = h->seed_base + (uint64_t)i * Gp;
+  }
+  std::vector<int> rc(ng, 0);
+  std::vector<std::string> err(ng);
+  std::vector<std::thread> th;
+  const double t0 = now_ms();
+  for (int i = 0; i < ng; ++i)
+    th.emplace_back([&, i]() {
+      rc[i] = mtaz_play(h->parts[i], Gp, 0);
+      if (rc[i] < 0) err[i] = mtaz_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int i = 0; i < ng; ++i)
+    if (rc[i] < 0) return set_err(rc[i], "group %d: %s", i, err[i].c_str());
+  h->rec.clear();
+  h->final_outcome.clear();
+  for (int i = 0; i < ST_COUNT; ++i) h->stats[i] = 0;
+  h->wave = 0;
+  for (mtaz_engine* p : h->parts) {
+    for (auto& r : p->rec) h->rec.push_back(std::move(r));
+    h->final_outcome.insert(h->final_outcome.end(), p->final_outcome.begin(), p->final_outcome.end());
+    for (int i = 0; i < ST_COUNT; ++i) {
+      if (i == ST_MAX_NODES || i == ST_MAX_EDGES || i == ST_NET_PREC || i == ST_MOVES)
+        h->stats[i] = std::max(h->stats[i], p->stats[i]);
+      else if (i != ST_WALL_MS) h->stats[i] += p->stats[i];
+    }
+    h->wave += p->wave;
+  }
+  h->stats[ST_WALL_MS] = now_ms() - t0;
+  h->n_played = h->G;
+  return 0;
+}
+
 extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
   if (n_games > h->G || n_games <= 0) return set_err(MTAZ_E_CAPACITY, "n_games=%d (engine has %d)", n_games, h->G);
+  if (h->groups > 1 && !from_current && n_games == h->G) return play_groups(h);
   HIPCHK(hipSetDevice(h->device));
   const double t0 = now_ms();
   const int G = h->G;

@@ -97,6 +97,11 @@ class Engine:
         bits pick A/B schedules of either kernel."""
         _lib.check(self.L.mtaz_set_net_variant(self.h, int(variant)))
 
+    def set_pipeline(self, groups):
+        """play() over `groups` independent game groups on their own HIP streams (1 = off).
+        Results are identical for any group count (games keep their global seeds)."""
+        _lib.check(self.L.mtaz_set_pipeline(self.h, int(groups)))
+
     def set_seed_base(self, seed_base):
         """Game slot g of the next play() uses np.random.seed(seed_base + g) semantics."""
         _lib.check(self.L.mtaz_set_seed_base(self.h, int(seed_base)))

@@ -132,3 +132,26 @@ def test_games_independent_of_batch_composition():
         one.set_weights(net)
         one.play()
         assert compare_records(one.episodes()[0], all_eps[g])[2] is None
+
+
+def test_pipelined_groups_equal_single_stream():
+    """mtaz_set_pipeline: game groups on separate HIP streams give the same episodes, in the
+    same game order, as one stream (the groups are disjoint global game ranges)."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    one = _engine(8, 8, seed_base=7)
+    one.set_weights(net)
+    one.play()
+    ref = one.episodes()
+    two = _engine(8, 8, seed_base=7)
+    two.set_weights(net)
+    for groups in (2, 4):
+        two.set_pipeline(groups)
+        st = two.play()
+        eps = two.episodes()
+        assert len(eps) == len(ref)
+        for g in range(len(ref)):
+            assert compare_records(eps[g], ref[g])[2] is None, (groups, g)
+        assert st['games'] == 8 and st['sims'] == one.stats()['sims']
