@@ -20,6 +20,31 @@ using namespace netc;
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int KBY = 72;   // k-blocks of 32 per conv
 
+// Mixed-precision FMAs (v_fma_mix*: each source f16 or f32).  The compiler does not form them
+// while f32 denormals are enabled, so they are written out.  Used only where the fused
+// result is exact in f32, hence bit-identical to the unfused expression:
+//  lo_pair: {f16(y0 - f32(h0)), f16(y1 - f32(h1))} packed, h = hi_pk (y - hi is exact in f32)
+//  mix_lo / mix_hi: fma(f32(f16 half of pk), b, c)
+__device__ __forceinline__ uint32_t lo_pair(uint32_t hi_pk, float y0, float y1) {
+  uint32_t r;
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(r)
+      : "v"(hi_pk), "v"(y0), "v"(y1));
+  return r;
+}
+__device__ __forceinline__ float mix_lo(uint32_t pk, float b, float c) {
+  float r;
+  asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(pk), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
+  float r;
+  asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(pk), "v"(b), "v"(c));
+  return r;
+}
+
 // one split pass over the wave's 32 tiles: W part WP (0 hi / 1 lo) x X part XP.
 // SA[2*ct + part], SB[part*8 + t] with t = 2*board + square tile.
 #define YMMA(SA, SB, WP, XP)                                                                          \
@@ -32,8 +57,8 @@ constexpr int KBY = 72;   // k-blocks of 32 per conv
 // Wh*Xh + Wh*Xl + Wl*Xh: 96 MFMAs, 31 independent ones between two updates of one accumulator
 #define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
 
-// VAR (in-process A/B, tools/bench_net.py): 0 = product schedule; 4, 16, 32, 64, 128: see the
-// trunk.  In-process A/B on one MI355X (4096 boards): 0 5.01 ms, 64 5.04, 128 5.06, 4 5.25-5.34.
+// VAR (in-process A/B, tools/bench_net.py): 0 = product; 4, 64, 128: K-loop schedules (see
+// the trunk); 1024: the epilogue in unfused form (bit-identity reference for the product).  In-process A/B on one MI355X (4096 boards): 0 5.01 ms, 64 5.04, 128 5.06, 4 5.25-5.34.
 template <bool STAMP, int VAR>
 __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
@@ -70,6 +95,9 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // Epilogue (stem and every conv): y = ReLU(acc * 2^-e + bias) written in place as f16
   // hi/lo; conv A seeds the accumulators with 2^e_next * x (conv B's residual), else resets.
   // Lane l holds channels 16ct + 4(l>>4) + r of square 16pt + (l&15): 8 B per image part.
+  // The lo parts and the residual seed use v_fma_mix (bit-identical to the unfused forms,
+  // test_mix_epilogue_bit_identical compared the two builds); the rest of the epilogue's time
+  // is the LDS writes of the new image (4 B per element).
   auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next) {
     constexpr bool conv_a = decltype(conv_a_t)::value;
     float ymax = 0.f;
@@ -89,23 +117,43 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
           y[1] = fmaxf(__builtin_fmaf(a[1], inv, bv.y), 0.f);
           y[2] = fmaxf(__builtin_fmaf(a[2], inv, bv.z), 0.f);
           y[3] = fmaxf(__builtin_fmaf(a[3], inv, bv.w), 0.f);
-          if constexpr (conv_a) {
-            const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
-            const f16x4 xl = *reinterpret_cast<const f16x4*>(smem + al);
+          if constexpr (VAR & 1024) {   // reference form of the same epilogue (unfused)
+            if constexpr (conv_a) {
+              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
+              const f16x4 xl = *reinterpret_cast<const f16x4*>(smem + al);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf((float)xh[j], s_next, (float)xl[j] * s_next);
+              for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf((float)xh[j], s_next, (float)xl[j] * s_next);
+            } else {
+              a = (f32x4v){0};
+            }
+            f16x4 yh, yl;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              ymax = fmaxf(ymax, y[j]);
+              yh[j] = (_Float16)y[j];
+              yl[j] = (_Float16)(y[j] - (float)yh[j]);
+            }
+            *reinterpret_cast<f16x4*>(smem + ah) = yh;
+            *reinterpret_cast<f16x4*>(smem + al) = yl;
+            continue;
+          }
+          if constexpr (conv_a) {
+            const uint2 xh = *reinterpret_cast<const uint2*>(smem + ah);
+            const uint2 xl = *reinterpret_cast<const uint2*>(smem + al);
+            a[0] = mix_lo(xh.x, s_next, mix_lo(xl.x, s_next, 0.f));
+            a[1] = mix_hi(xh.x, s_next, mix_hi(xl.x, s_next, 0.f));
+            a[2] = mix_lo(xh.y, s_next, mix_lo(xl.y, s_next, 0.f));
+            a[3] = mix_hi(xh.y, s_next, mix_hi(xl.y, s_next, 0.f));
           } else {
             a = (f32x4v){0};
           }
-          f16x4 yh, yl;
+          ymax = fmaxf(fmaxf(ymax, fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
+          f16x4 yh;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            ymax = fmaxf(ymax, y[j]);
-            yh[j] = (_Float16)y[j];
-            yl[j] = (_Float16)__builtin_fmaf((float)yh[j], -1.f, y[j]);
-          }
-          *reinterpret_cast<f16x4*>(smem + ah) = yh;
-          *reinterpret_cast<f16x4*>(smem + al) = yl;
+          for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
+          const uint2 hp = __builtin_bit_cast(uint2, yh);
+          *reinterpret_cast<uint2*>(smem + ah) = hp;
+          *reinterpret_cast<uint2*>(smem + al) = make_uint2(lo_pair(hp.x, y[0], y[1]), lo_pair(hp.y, y[2], y[3]));
         } else {
           a = (f32x4v){0};
         }
@@ -150,9 +198,8 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // schedule, STEP below).  Variants 128 / 64 run each step as two half-steps, one per square
   // tile, so only 8 activation fragments are live (a 2 x 8-fragment ring): 128 with
   // sched_group_barrier, 64 with the order pinned by sched_barrier (no accumulator copies).
-  // variant 32: weights one k-block ahead (2-slot ring, unroll 2) for lower register pressure
   constexpr bool HALVES = (VAR & (64 | 128)) != 0;
-  constexpr int PD = (VAR & 32) ? 1 : 2, RS = PD + 1, U = (VAR & 32) ? 2 : 6;
+  constexpr int PD = 2, RS = 3, U = 6;
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
   f16x8 A[RS][8], B[2][16], BH[2][8];
   const uint4* Wl = W.convy + (size_t)(4 * wave) * KBY * 128 + lane;
@@ -258,8 +305,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   }
 // Whole-k-block steps.  Product: the next k-block's 16 LDS reads one per 2 MFMAs at the top
 // of the step, then the 8 weight loads one per 4 MFMAs, then 32 MFMAs.  Variants: 4 = all
-// loads first, then the 96 MFMAs; 16 = the Wh*Xl pass first so the next Xl reuses its
-// registers.
+// loads first, then the 96 MFMAs.
 #define STEP(KB, AC, AP, BC, BP)                                   \
   if constexpr (VAR & 4) {                                         \
     LOAD_B(BP, (KB) + 1);                                          \
@@ -267,30 +313,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     __builtin_amdgcn_sched_barrier(0);                             \
     YMMA3(AC, BC);                                                 \
     __builtin_amdgcn_sched_barrier(0);                             \
-  } else if constexpr (VAR & 16) {                                 \
-    /* Wh*Xl first: Xl(kb) dies after a third of the step and Xl(kb+1) reuses it */ \
-    YMMA(AC, BC, 0, 1);                                            \
-    LOAD_BP(BP, (KB) + 1, 0);                                      \
-    LOAD_A(AP, (KB) + PD);                                         \
-    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           \
-    }                                                              \
-    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);           \
-    }                                                              \
-    __builtin_amdgcn_sched_barrier(0);                             \
-    YMMA(AC, BC, 0, 0);                                            \
-    LOAD_BP(BP, (KB) + 1, 1);                                      \
-    YMMA(AC, BC, 1, 0);                                            \
-    _Pragma("unroll") for (int g_ = 0; g_ < 8; ++g_) {             \
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);           \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);           \
-    }                                                              \
-    __builtin_amdgcn_sched_group_barrier(0x008, 48, 0);            \
-    __builtin_amdgcn_sched_barrier(0);                             \
-  } else {   /* product, VAR 32 */                                  \
+  } else {   /* product */                                          \
     LOAD_B(BP, (KB) + 1);                                          \
     LOAD_A(AP, (KB) + PD);                                         \
     YMMA3(AC, BC);                                                 \
@@ -370,16 +393,14 @@ template <bool S>
 static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
-  if (var & 64)
+  if (var == 1024)
+    hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 64)
     hipLaunchKernelGGL((k_net_y<S, 64>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 128)
     hipLaunchKernelGGL((k_net_y<S, 128>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var & 32)
-    hipLaunchKernelGGL((k_net_y<S, 32>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 4)
     hipLaunchKernelGGL((k_net_y<S, 4>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var & 16)
-    hipLaunchKernelGGL((k_net_y<S, 16>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else
     hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
 }

@@ -87,3 +87,23 @@ def test_net_vs_torch_cpu_many_positions(engine):
             worst = max(worst, float(np.max(np.abs(p[0].numpy() - logits[i]))))
             assert abs(float(v.item()) - float(values[i])) <= VALUE_TOL
     assert worst <= LOGIT_TOL
+
+
+def test_mix_epilogue_bit_identical():
+    """k_net_y's product epilogue (v_fma_mix forms) stores exactly the bits of the unfused
+    expressions (variant 1024): logits and values of the two builds must be bitwise equal."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from minitchess_alphazero_amd.network import Network
+    from tests_positions import random_fens
+    import torch
+    eng = Engine(n_games=64, sims=8)
+    torch.manual_seed(0)
+    eng.set_weights(Network())
+    pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=5)])
+    eng.set_net_variant(0)
+    l0, v0 = eng.evaluate(pos)
+    eng.set_net_variant(1024)
+    l1, v1 = eng.evaluate(pos)
+    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
