@@ -130,6 +130,10 @@ struct NetWeights {
   // stem: [cotile 16][kblock 3][part][lane 64][8 x f16], co = 16*cotile + (l&15),
   // tap = 4*kblock + (l>>4) (taps 9..11 zero), channel j; scale stemx_inv
   const uint4* stemy;
+  // k_net_y dynamic range: [2L] = max over output channels of the L1 norm of conv L's folded
+  // weights, [2L+1] = max |folded bias| (L < 18); [36], [37] the same for the stem; [38] =
+  // max |embedding|.  Each rounded up to float.
+  const float* yrange;
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304

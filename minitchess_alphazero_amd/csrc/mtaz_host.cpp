@@ -470,6 +470,7 @@ struct mtaz_engine {
   int variant = 0;   // fp16x3 network kernel variant (0 = product k_net_y; NET_VAR_X = k_net_x)
   uint4* wxbuf = nullptr;
   float* wxinv = nullptr;
+  float* wyrange = nullptr;
   std::vector<void*> allocs;
   float* wbuf = nullptr;
   // scratch
@@ -839,6 +840,36 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             }
             sy[((((size_t)ct * 3 + kb) * 2 + part) * 64 + lane) * 8 + j] = v;
           }
+  // k_net_y output bounds (NetWeights::yrange): per conv the max over output channels of the
+  // L1 norm of the folded weights and the max |folded bias|; the stem's; max |embedding|.
+  std::vector<float> yr(2 * CONV_LAYERS + 3);
+  auto up = [](double d) {   // float >= d
+    float f = (float)d;
+    if ((double)f < d) f = std::nextafter(f, INFINITY);
+    return f;
+  };
+  for (int L = 0; L <= CONV_LAYERS; ++L) {
+    const bool stem = L == CONV_LAYERS;
+    const int base = stem ? 1 : 7 + L * 6, kk = stem ? 72 : 2304;
+    fold(base, 256, sc, sh);
+    double g = 0, b = 0;
+    for (int co = 0; co < 256; ++co) {
+      double r = 0;
+      for (int j = 0; j < kk; ++j) r += fabs((double)t[base][(size_t)co * kk + j]);
+      g = std::max(g, r * fabs(sc[co]));
+      b = std::max(b, fabs(sh[co]));
+    }
+    yr[2 * L] = up(g);
+    yr[2 * L + 1] = up(b);
+  }
+  {
+    double e = 0;
+    for (float v : t[0]) e = std::max(e, fabs((double)v));
+    yr[2 * CONV_LAYERS + 2] = up(e);
+  }
+  if (!h->wyrange) ECHK(h->dalloc(&h->wyrange, yr.size()));
+  HIPCHK(hipMemcpy(h->wyrange, yr.data(), yr.size() * 4, hipMemcpyHostToDevice));
+  h->w.yrange = h->wyrange;
   const size_t nx = wx.size() / 8, ns = sx.size() / 8, nsy = sy.size() / 8;
   if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, 2 * nx + ns + nsy));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));

@@ -57,8 +57,10 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
 // Wh*Xh + Wh*Xl + Wl*Xh: 96 MFMAs, 31 independent ones between two updates of one accumulator
 #define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
 
-// VAR (in-process A/B, tools/bench_net.py): 0 = product; 4, 64, 128: K-loop schedules (see
-// the trunk); 1024: the epilogue in unfused form (bit-identity reference for the product).  In-process A/B on one MI355X (4096 boards): 0 5.01 ms, 64 5.04, 128 5.06, 4 5.25-5.34.
+// VAR (in-process A/B, tools/bench_net.py): 0 = product; 4, 8, 128: K-loop schedules (see the
+// trunk); 1024: the epilogue in unfused form (bit-identity reference for the product).
+// In-process A/B on one MI355X, 4096 boards, before dynamic range: pinned half-steps (now 0)
+// 5.04 ms, whole steps (now 8) 5.01, 128 5.06, 4 5.25-5.34.
 template <bool STAMP, int VAR>
 __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
@@ -92,19 +94,43 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   for (int i = 0; i < 32; ++i) acc[i] = (f32x4v){0};
   int overflow = 0;
 
-  // Epilogue (stem and every conv): y = ReLU(acc * 2^-e + bias) written in place as f16
-  // hi/lo; conv A seeds the accumulators with 2^e_next * x (conv B's residual), else resets.
-  // Lane l holds channels 16ct + 4(l>>4) + r of square 16pt + (l&15): 8 B per image part.
-  // The lo parts and the residual seed use v_fma_mix (bit-identical to the unfused forms,
-  // test_mix_epilogue_bit_identical compared the two builds); the rest of the epilogue's time
-  // is the LDS writes of the new image (4 B per element).
-  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next) {
+  // Dynamic range.  The image holds x * 2^-xs in f16 hi/lo with one exponent xs per workgroup
+  // (uniform), so activations keep fp32's range (a freshly trained net in eval mode can grow
+  // far beyond f16's 65504) at f16x3 precision.  xs is chosen BEFORE a layer's outputs are
+  // stored, from a rigorous bound on them: |z| <= G_L * max(input) + B_L (+ max(residual) for
+  // conv B), G_L = max over output channels of the L1 norm of the folded weights, B_L = max
+  // |folded bias| (host, NetWeights::yrange), and max(input) measured by the previous epilogue
+  // (workgroup max of its outputs through one LDS word).  xo = max(0, ilogb(bound) - 14) keeps
+  // every stored value below 2^15; rescaling is by powers of two, hence exact, and ordinary nets
+  // stay at xs = 0 (the results are then bit-identical to an unscaled kernel).
+  int xs = 0;
+  float mx_img = W.yrange[2 * CONV_LAYERS + 2];   // max |embedding| = max of the stem input
+  float mx_blk = 0.f;                             // max of the current residual block's input
+  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMGB + AUXB - 16);
+  if (tid == 0) mxs[0] = mxs[1] = 0u;
+  int slot = 0;
+
+  // Epilogue (stem and every conv): y = ReLU(acc * 2^(xs - e) + bias) stored in place as f16
+  // hi/lo of y * 2^-xo (the scale folded into the fma); conv A seeds the accumulators with conv B's residual in conv B's units
+  // (x_stored * 2^(e_B + xs - xo)), otherwise resets them.  Lane l holds channels
+  // 16ct + 4(l>>4) + r of square 16pt + (l&15): 8 B per image part.  The lo parts and the
+  // residual seed use v_fma_mix (bit-identical to the unfused forms, variant 1024;
+  // test_mix_epilogue_bit_identical).  Ends with a barrier, after which mx_img holds the
+  // workgroup max of the new image (true units).
+  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next, float bound) {
     constexpr bool conv_a = decltype(conv_a_t)::value;
+    // floor(log2(bound)) - 14 for bound >= 2^14 (exponent field of a normal float); inf -> 114
+    const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
+    // stored y = ReLU(acc * 2^(xs - e - xo) + bias * 2^-xo): the power-of-two output scale folded
+    // into the fma (exact, so the same bits as scaling y afterwards)
+    const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
+    const float sseed = __builtin_ldexpf(s_next, xs - xo);
     float ymax = 0.f;
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       const int co0 = 64 * wave + 16 * ct + 4 * g;
-      const float4 bv = *reinterpret_cast<const float4*>(bias + co0);
+      const float4 bu = *reinterpret_cast<const float4*>(bias + co0);
+      const float4 bv = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const int bb = t >> 1, pt = t & 1;
@@ -113,23 +139,23 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
           const int p = pt ? p1 : n;
           const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1), al = ah + PARTB;
           float y[4];
-          y[0] = fmaxf(__builtin_fmaf(a[0], inv, bv.x), 0.f);
-          y[1] = fmaxf(__builtin_fmaf(a[1], inv, bv.y), 0.f);
-          y[2] = fmaxf(__builtin_fmaf(a[2], inv, bv.z), 0.f);
-          y[3] = fmaxf(__builtin_fmaf(a[3], inv, bv.w), 0.f);
+          y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
+          y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
+          y[2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv.z), 0.f);
+          y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
+          ymax = fmaxf(fmaxf(ymax, fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));   // stored units
           if constexpr (VAR & 1024) {   // reference form of the same epilogue (unfused)
             if constexpr (conv_a) {
               const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
               const f16x4 xl = *reinterpret_cast<const f16x4*>(smem + al);
 #pragma unroll
-              for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf((float)xh[j], s_next, (float)xl[j] * s_next);
+              for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf((float)xh[j], sseed, (float)xl[j] * sseed);
             } else {
               a = (f32x4v){0};
             }
             f16x4 yh, yl;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              ymax = fmaxf(ymax, y[j]);
               yh[j] = (_Float16)y[j];
               yl[j] = (_Float16)(y[j] - (float)yh[j]);
             }
@@ -140,14 +166,13 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
           if constexpr (conv_a) {
             const uint2 xh = *reinterpret_cast<const uint2*>(smem + ah);
             const uint2 xl = *reinterpret_cast<const uint2*>(smem + al);
-            a[0] = mix_lo(xh.x, s_next, mix_lo(xl.x, s_next, 0.f));
-            a[1] = mix_hi(xh.x, s_next, mix_hi(xl.x, s_next, 0.f));
-            a[2] = mix_lo(xh.y, s_next, mix_lo(xl.y, s_next, 0.f));
-            a[3] = mix_hi(xh.y, s_next, mix_hi(xl.y, s_next, 0.f));
+            a[0] = mix_lo(xh.x, sseed, mix_lo(xl.x, sseed, 0.f));
+            a[1] = mix_hi(xh.x, sseed, mix_hi(xl.x, sseed, 0.f));
+            a[2] = mix_lo(xh.y, sseed, mix_lo(xl.y, sseed, 0.f));
+            a[3] = mix_hi(xh.y, sseed, mix_hi(xl.y, sseed, 0.f));
           } else {
             a = (f32x4v){0};
           }
-          ymax = fmaxf(fmaxf(ymax, fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
           f16x4 yh;
 #pragma unroll
           for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
@@ -159,7 +184,16 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         }
       }
     }
-    overflow |= ymax >= 65504.f;
+    // workgroup max of the new image (y >= 0: float bits order as values; NaN above +inf)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o, 64));
+    if (lane == 0) atomicMax(&mxs[slot], __float_as_uint(ymax));
+    if (tid == 0) mxs[slot ^ 1] = 0u;   // every wave read it before this epilogue's first barrier
+    xs = xo;
+    __syncthreads();
+    mx_img = __builtin_ldexpf(__uint_as_float(mxs[slot]), xo);   // true units
+    slot ^= 1;
+    if (!__builtin_isfinite(mx_img)) overflow = 1;   // fp32 overflow / NaN, as fp32 would produce
   };
 
   // ---------------- stem: conv3x3 8->256, K = 3 k-blocks of (4 taps x 8 channels) ----------
@@ -188,17 +222,18 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       YMMA3(SA, SB);
     }
   }
-  epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f);
-  __syncthreads();
+  epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f,
+           __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mx_img, W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f);
   stamp(st_stem);
 
   // ---------------- residual trunk: 18 convs, activations resident in LDS ----------------
-  // Weights stream from L2 through a 3-slot register ring two k-blocks ahead; the next
-  // k-block's 16 activation fragments are read from LDS during the current step (product
-  // schedule, STEP below).  Variants 128 / 64 run each step as two half-steps, one per square
-  // tile, so only 8 activation fragments are live (a 2 x 8-fragment ring): 128 with
-  // sched_group_barrier, 64 with the order pinned by sched_barrier (no accumulator copies).
-  constexpr bool HALVES = (VAR & (64 | 128)) != 0;
+  // Weights stream from L2 through a 3-slot register ring two k-blocks ahead.  Product
+  // schedule: each k-block step runs as two half-steps, one per square tile, so only the 8
+  // activation fragments of one tile are live (a 2 x 8-fragment ring): the next half's are read
+  // from LDS during the current half, in 12 chunks of 4 MFMAs whose order sched_barrier pins
+  // (HALF_PINNED: no accumulator copies, no spills).  Variants: 128 = the same half-steps
+  // scheduled by sched_group_barrier; 8 / 4 = whole-k-block steps (STEP).
+  constexpr bool HALVES = (VAR & (4 | 8)) == 0;
   constexpr int PD = 2, RS = 3, U = 6;
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
   f16x8 A[RS][8], B[2][16], BH[2][8];
@@ -254,9 +289,8 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(                         \
           SA[2 * ct_ + (WP)], SB[(XP) * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0);             \
   }
-// variant 64: the same half-step in 12 chunks of 4 MFMAs in fixed program order
-// (sched_barrier between chunks), LDS reads 2 per chunk in chunks 0-3, weight loads 1 per
-// chunk in chunks 4-7
+// product half-step: 12 chunks of 4 MFMAs in fixed program order (sched_barrier between
+// chunks), LDS reads 2 per chunk in chunks 0-3, weight loads 1 per chunk in chunks 4-7
 #define HALF_PINNED(KB, PT, AC, AP, BC, BN, KBN, PTN)                                 \
   {                                                                                   \
     const int kk_ = (KBN) < KBY ? (KBN) : KBY - 1;                                    \
@@ -303,9 +337,9 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);            \
     __builtin_amdgcn_sched_barrier(0);                             \
   }
-// Whole-k-block steps.  Product: the next k-block's 16 LDS reads one per 2 MFMAs at the top
-// of the step, then the 8 weight loads one per 4 MFMAs, then 32 MFMAs.  Variants: 4 = all
-// loads first, then the 96 MFMAs.
+// Whole-k-block steps.  Variant 8: the next k-block's 16 LDS reads one per 2 MFMAs at the top
+// of the step, then the 8 weight loads one per 4 MFMAs, then 32 MFMAs; variant 4: all loads
+// first, then the 96 MFMAs.
 #define STEP(KB, AC, AP, BC, BP)                                   \
   if constexpr (VAR & 4) {                                         \
     LOAD_B(BP, (KB) + 1);                                          \
@@ -313,7 +347,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     __builtin_amdgcn_sched_barrier(0);                             \
     YMMA3(AC, BC);                                                 \
     __builtin_amdgcn_sched_barrier(0);                             \
-  } else {   /* product */                                          \
+  } else {   /* VAR 8 */                                            \
     LOAD_B(BP, (KB) + 1);                                          \
     LOAD_A(AP, (KB) + PD);                                         \
     YMMA3(AC, BC);                                                 \
@@ -336,7 +370,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       for (int kb = 0; kb < KBY; kb += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if constexpr (VAR & 64) {
+          if constexpr (!(VAR & 128)) {
             HALF_PINNED(kb + u, 0, A[u % RS], A[(u + PD) % RS], BH[0], BH[1], kb + u, 1);
             HALF_PINNED(kb + u, 1, A[u % RS], A[(u + PD) % RS], BH[1], BH[0], kb + u + 1, 0);
           } else {
@@ -355,11 +389,15 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     stamp(st_k);
     Wl += CONVX_U4_PER_LAYER;
     __syncthreads();   // every wave has finished reading this layer's input image
-    if ((L & 1) == 0)
-      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1]);
-    else
-      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f);
-    __syncthreads();
+    // output bound (the margin 1 + 2^-10 covers the rounding of the bound's own arithmetic)
+    if ((L & 1) == 0) {
+      const float bound = __builtin_fmaf(W.yrange[2 * L], mx_img, W.yrange[2 * L + 1]) * 1.0009765625f;
+      mx_blk = mx_img;
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bound);
+    } else {
+      const float bound = (__builtin_fmaf(W.yrange[2 * L], mx_img, W.yrange[2 * L + 1]) + mx_blk) * 1.0009765625f;
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bound);
+    }
     stamp(st_epi);
   }
 #undef STEP
@@ -374,7 +412,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   if (overflow) atomicOr(D.pr.err, ERR_F16);
 
   // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
-  heads_reduce(smem, pos, b0, nb, W, tid);
+  heads_reduce(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs));
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
@@ -395,8 +433,8 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      unsigned long long* stamps) {
   if (var == 1024)
     hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var & 64)
-    hipLaunchKernelGGL((k_net_y<S, 64>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 8)
+    hipLaunchKernelGGL((k_net_y<S, 8>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 128)
     hipLaunchKernelGGL((k_net_y<S, 128>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 4)

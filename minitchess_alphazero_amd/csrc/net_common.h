@@ -87,8 +87,9 @@ __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* po
 // Heads, part 1 (all 256 threads): policy conv 256->2 and value conv 256->1 (1x1, BN folded,
 // ReLU) from the final image, the clock feature, the value MLP hidden layer and its
 // reduction.  Leaves fp [XB][64] (60 policy features + clock), red[bb*256] = value pre-tanh.
+// xscale: the image holds x / xscale (a power of two; k_net_y's dynamic range), 1 otherwise.
 __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0, int nb, const NetWeights& W,
-                                             int tid) {
+                                             int tid, float xscale = 1.f) {
   float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
   float* fv = fp + XB * 64;                            // [XB][32]: vconv features (30) + clock
   float* red = fv + XB * 32;                           // [XB][256]
@@ -102,7 +103,7 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += wr[8 * c + j] * ((float)xh[j] + (float)xl[j]);
     }
-    s = fmaxf(s + (o < 2 ? W.pconv_b[o] : W.vconv_b[0]), 0.f);
+    s = fmaxf(__builtin_fmaf(s, xscale, o < 2 ? W.pconv_b[o] : W.vconv_b[0]), 0.f);
     if (o < 2) fp[bb * 64 + o * 30 + p] = s; else fv[bb * 32 + p] = s;
   }
   if (tid < XB) {

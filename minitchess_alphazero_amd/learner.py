@@ -1,0 +1,253 @@
+"""Learner: drop-in for exp/learner.py, exp/dataset.py and LearnPuppet (app/base.py:137-205).
+
+SURVEY 8f rank 1.  Training is the reference's update on PyTorch-ROCm autograd (SURVEY 8f:
+"PyTorch-ROCm autograd is acceptable here"): the same loss (exp/learner.py:86-87), a fresh
+AdamW(**optim_params) per update (:71-72), a shuffled pass over the dataset in batches of
+`batch_size` (:73-76), `epochs` passes, train-mode BatchNorm.
+
+What differs is how batches are built.  The reference collates every batch on the host from
+FEN strings (:23-41).  Here the whole dataset is encoded once per update: the positions
+are parsed by libmtaz, the tokens and clocks come from the HIP batch encoder
+(mtaz_encode_batch, the kernel that feeds self-play), and the dense pi targets are built
+with numpy.  These tensors stay resident on the GPU.  Each batch is an index gather in
+the order the reference's DataLoader would draw: the same RandomSampler on torch's global
+RNG, so a seeded update visits the rows in the same order.  `collate_fn` is kept with the
+reference's signature and output for callers that use a DataLoader themselves.
+
+MQTT / HTTP transport (app/learner.py) is out of scope (wire formats are rank 3);
+LearnPuppet keeps the state machine, the dataset and the versioned weights.
+"""
+import copy
+import logging
+from collections import deque
+from datetime import datetime
+
+import numpy as np
+import torch
+
+from . import _lib
+from .environment import pos_encode, pos_from_fen
+from .network import NUM_ACTIONS, Network
+from .puppet import MasterOfPuppetsStatus
+
+log = logging.getLogger(__name__)
+
+
+# ---- dataset (exp/dataset.py:6-20) --------------------------------------------------------------
+class SimpleAlphaZeroDataset(torch.utils.data.Dataset):
+    """Replay memory of self-play rows {'observation', 'legal_moves', 'pi', 'reward'}: a
+    deque of max_length rows; push() extends it (oldest rows fall out)."""
+
+    def __init__(self, max_length):
+        self._memory = deque(maxlen=max_length)
+
+    def get_memory(self):
+        return list(self._memory)
+
+    def push(self, data):
+        self._memory.extend(data)
+
+    def __len__(self):
+        return len(self._memory)
+
+    def __getitem__(self, i):
+        return self._memory[i]
+
+
+# ---- batch construction ---------------------------------------------------------------------------
+def dense_pi(rows):
+    """pi targets [n, 554] float32: pi[legal_moves] = pi (float32), a code that repeats in
+    the legal list (promotions) keeps its last value (exp/learner.py:29-30)."""
+    out = np.zeros((len(rows), NUM_ACTIONS), np.float32)
+    for i, r in enumerate(rows):
+        out[i, np.asarray(r['legal_moves'], np.int64)] = np.asarray(r['pi'], np.float64).astype(np.float32)
+    return out
+
+
+def collate_fn(batch):
+    """exp/learner.py:23-41: (pi [B,554] f32, tokens [B,2,6,5] i64, clock [B,1] f32, reward [B,1] f32)."""
+    toks, clocks = [], []
+    for r in batch:
+        t, c = pos_encode(pos_from_fen(r['observation']))
+        toks.append(t)
+        clocks.append(c)
+    return (torch.from_numpy(dense_pi(batch)), torch.from_numpy(np.stack(toks)).reshape(-1, 2, 6, 5),
+            torch.tensor(np.asarray(clocks, np.float32)).reshape(-1, 1),
+            torch.tensor(np.asarray([float(r['reward']) for r in batch], np.float32)).reshape(-1, 1))
+
+
+def encode_positions(pos, device):
+    """Packed positions [n, 5] u32 -> tokens [n,2,6,5] int64 and clock [n,1] f32 on `device`,
+    by the HIP batch encoder (exp/policy.py:96-105 for the whole batch in one launch)."""
+    dev = torch.device(device)
+    d_pos = torch.from_numpy(np.ascontiguousarray(pos, np.uint32).view(np.int32)).to(dev)
+    n = d_pos.shape[0]
+    tok = torch.empty((n, 60), dtype=torch.uint8, device=dev)
+    clk = torch.empty((n,), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)
+    _lib.check(_lib.lib().mtaz_encode_batch(dev.index or 0, d_pos.data_ptr(), n, tok.data_ptr(), clk.data_ptr(), None))
+    torch.cuda.synchronize(dev)
+    return tok.long().reshape(n, 2, 6, 5), clk.reshape(n, 1)
+
+
+class ResidentBatches:
+    """A dataset encoded once and kept on the device; batches are index gathers."""
+
+    def __init__(self, rows, device):
+        self.device = torch.device(device)
+        pos = np.stack([pos_from_fen(r['observation']) for r in rows]) if rows else np.zeros((0, 5), np.uint32)
+        if self.device.type == 'cuda':
+            self.tokens, self.clock = encode_positions(pos, self.device)
+        else:   # host encoder (CPU tests; the product learner runs on the GPU)
+            enc = [pos_encode(p) for p in pos]
+            self.tokens = torch.from_numpy(np.stack([t for t, _ in enc])).reshape(-1, 2, 6, 5)
+            self.clock = torch.tensor(np.asarray([c for _, c in enc], np.float32)).reshape(-1, 1)
+        self.pi = torch.from_numpy(dense_pi(rows)).to(self.device)
+        self.reward = torch.tensor(np.asarray([float(r['reward']) for r in rows], np.float32)).reshape(-1, 1).to(self.device)
+
+    def __len__(self):
+        return self.pi.shape[0]
+
+    def batch(self, idx):
+        i = torch.as_tensor(idx, dtype=torch.long, device=self.device)
+        return self.pi[i], self.tokens[i], self.clock[i], self.reward[i]
+
+
+def sampler_order(n):
+    """The row order a DataLoader(shuffle=True) draws for an n-row dataset, consuming torch's
+    global generator as the reference's DataLoader does: the iterator first draws its worker
+    base seed, then RandomSampler draws the seed of its own generator for randperm
+    (tests/test_learner_cpu.py checks the order against a real DataLoader)."""
+    torch.empty((), dtype=torch.int64).random_()
+    return list(iter(torch.utils.data.RandomSampler(range(n))))
+
+
+# ---- loss / metric (exp/learner.py:44-59, :84-88) --------------------------------------------------
+class AvgSmoothLoss:
+    def __init__(self, beta=0.98):
+        self.beta = beta
+        self.count, self.val = 0, 0.0
+
+    def reset(self):
+        self.count, self.val = 0, 0.0
+        return self
+
+    def accumulate(self, new_val):
+        self.count += 1
+        self.val = new_val + self.beta * (self.val - new_val)
+
+    @property
+    def value(self):
+        return self.val / (1 - self.beta ** self.count)
+
+
+def alphazero_loss(model, pib, tokens, clock, reward):
+    """mean((v - r)^2 - sum(pi * log_softmax(p)))  (exp/learner.py:86-87)"""
+    p, v = model((tokens, clock))
+    return ((v - reward) ** 2 - (pib * p.log_softmax(-1)).sum(1)).mean()
+
+
+# ---- learner (exp/learner.py:62-91) ------------------------------------------------------------------
+class SimpleAlphaZeroLearner:
+    def __init__(self, env, num_simulations, network, batch_size, epochs, optim_params, device=None):
+        self._env = env
+        self._num_simulations = num_simulations
+        self._network = network
+        self._batch_size = batch_size
+        self._epochs = epochs
+        self._optim_params = dict(optim_params)
+        self._device = torch.device(device) if device is not None else \
+            torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available() else torch.device('cpu')
+        self.last_losses = []
+
+    def update(self, dataset):
+        """One learner update over `dataset` (rows or SimpleAlphaZeroDataset).  Returns the
+        smoothed loss; per-batch values in self.last_losses."""
+        rows = dataset.get_memory() if hasattr(dataset, 'get_memory') else list(dataset)
+        model = self._network.train().to(self._device)
+        optimizer = torch.optim.AdamW(model.parameters(), **self._optim_params)
+        data = ResidentBatches(rows, self._device)
+        metric = AvgSmoothLoss().reset()
+        losses = []
+        for epoch in range(self._epochs):
+            order = sampler_order(len(data))
+            for s in range(0, len(order), self._batch_size):
+                pib, tok, clk, rew = data.batch(order[s:s + self._batch_size])
+                loss = alphazero_loss(model, pib, tok, clk, rew)
+                optimizer.zero_grad()
+                loss.backward()
+                lv = float(loss.detach().item())
+                metric.accumulate(lv)
+                losses.append(lv)
+                optimizer.step()
+            log.info('Epoch %d: %.2f', epoch, metric.value if metric.count else float('nan'))
+        self.last_losses = losses
+        return metric.value if metric.count else float('nan')
+
+
+# ---- LearnPuppet (app/base.py:137-205, transport excluded) --------------------------------------------
+class LearnPuppet:
+    def __init__(self, userid, batch_size, epochs, optim_params, device=None, max_length=1_000_000):
+        self._userid = userid
+        self._max_length = max_length
+        self._dataset = None
+        self._init_dataset()
+        self._network = Network()
+        self._learner = SimpleAlphaZeroLearner(None, 36, self._network, batch_size, epochs, optim_params, device)
+        self._episode_counter = 0
+        self._weights_version = None
+        self._weights = None
+        self.weights = self._network.state_dict()
+        self._status = MasterOfPuppetsStatus.SIMULATE
+
+    def _init_dataset(self):
+        self._dataset = SimpleAlphaZeroDataset(max_length=self._max_length)
+
+    @property
+    def episode_counter(self):
+        return self._episode_counter
+
+    @property
+    def weights_version(self):
+        return self._weights_version
+
+    @property
+    def weights(self):
+        return self._weights
+
+    @weights.setter
+    def weights(self, value):
+        self._weights = {k: v.detach().cpu().clone() for k, v in value.items()}
+        self._weights_version = datetime.now().strftime('%Y%m%d%H%M%S')
+
+    @property
+    def status(self):
+        return self._status.name
+
+    def train(self):
+        self._status = MasterOfPuppetsStatus.TRAIN
+
+    def simulate(self):
+        self._status = MasterOfPuppetsStatus.SIMULATE
+
+    def push_data(self, data):
+        """One episode's rows (app/learner.py:54 -> app/base.py:182-185)."""
+        if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
+            self._episode_counter += 1
+            self._dataset.push(data)
+
+    def update(self):
+        """app/base.py:188-195: load the current weights, train on the dataset, publish the new
+        weights as a new version, start a fresh dataset."""
+        self._network.load_state_dict(self.weights)
+        loss = self._learner.update(self._dataset)
+        self.weights = self._network.state_dict()
+        self._init_dataset()
+        out = self.get_weights_dict()
+        out['loss'] = loss
+        return out
+
+    def get_weights_dict(self):
+        """{'weights': state_dict (CPU tensors), 'version'}; the reference jsonpickle-encodes the
+        state_dict for HTTP (app/base.py:201-203) - the wire format is SURVEY 8f rank 3."""
+        return {'weights': copy.copy(self.weights), 'version': self.weights_version}

@@ -1,12 +1,14 @@
-"""Policy/value network parameters: drop-in for exp/policy.py's Network as a weight container.
+"""Policy/value network: drop-in for exp/policy.py's Network.
 
-PyTorch holds the parameters only (device memory + the state_dict format the
-reference's learner/rlweb exchange, app/base.py:126-129, :171-174).  Parameter
-creation order and state_dict keys equal the reference's (exp/policy.py:53-69),
-so `torch.manual_seed(0); Network()` yields the reference's random-init weights
-and `load_state_dict` accepts reference checkpoints.  Inference runs in the HIP
-kernels (csrc/mtaz_device.hip) through Engine.set_weights / Engine.evaluate;
-there is no torch forward on the product path.
+Parameter creation order and state_dict keys equal the reference's
+(exp/policy.py:53-69), so `torch.manual_seed(0); Network()` yields the reference's
+random-init weights and `load_state_dict` accepts reference checkpoints.
+
+Self-play inference does not use this module's forward: it runs in the HIP kernels
+(k_net_y, csrc/mtaz_net16.hip) through Engine.set_weights / Engine.evaluate.  The torch
+forward below is the TRAINING path of the learner (exp/learner.py:84-88; autograd on
+PyTorch-ROCm): train-mode BatchNorm uses batch statistics, which the folded
+inference kernels cannot express.
 """
 import torch
 from torch import nn
@@ -16,21 +18,35 @@ EMBEDDING_DIM = 4
 MAX_NUM_MOVES_ALLOWED = 30
 
 
+class _ConvBN(nn.Module):
+    """exp/policy.py:15-38 ConvBlock: Conv2d(k, pad k//2) -> BatchNorm2d [-> ReLU]."""
+
+    def __init__(self, cin, cout, k, relu=True):
+        super().__init__()
+        mods = [nn.Conv2d(cin, cout, kernel_size=k, stride=1, padding=k // 2), nn.BatchNorm2d(cout)]
+        if relu:
+            mods.append(nn.ReLU())
+        self.layers = nn.Sequential(*mods)
+
+    def forward(self, x):
+        return self.layers(x)
+
+
 def _conv_bn(cin, cout, k, relu=True):
-    m = nn.Module()
-    mods = [nn.Conv2d(cin, cout, kernel_size=k, stride=1, padding=k // 2), nn.BatchNorm2d(cout)]
-    if relu:
-        mods.append(nn.ReLU())
-    m.layers = nn.Sequential(*mods)
-    return m
+    return _ConvBN(cin, cout, k, relu)
 
 
 class _Residual(nn.Module):
+    """exp/policy.py:41-50: relu(convblock2(convblock1(x)) + x)."""
+
     def __init__(self, ch):
         super().__init__()
         self.convblock1 = _conv_bn(ch, ch, 3)
         self.convblock2 = _conv_bn(ch, ch, 3, relu=False)
         self.nonl = nn.ReLU()
+
+    def forward(self, x):
+        return self.nonl(self.convblock2(self.convblock1(x)) + x)
 
 
 class Network(nn.Module):
@@ -43,8 +59,15 @@ class Network(nn.Module):
         self.vconv = _conv_bn(256, 1, 1)
         self.vlinear = nn.Sequential(nn.Linear(6 * 5 + 1, 256), nn.ReLU(), nn.Linear(256, 1), nn.Tanh())
 
-    def forward(self, *a, **k):
-        raise NotImplementedError('inference runs in the HIP engine: use Engine.evaluate / Engine.play')
+    def forward(self, input_data):
+        """Training forward (exp/policy.py:71-80): tokens (B,2,6,5) int64, clock (B,1) ->
+        (logits (B,554), value (B,1))."""
+        tokens, clock = input_data
+        x = self.emb(tokens).permute(0, 1, 4, 2, 3).reshape(-1, 2 * EMBEDDING_DIM, 6, 5)
+        x = self.resbody(x)
+        logits = self.plinear(torch.cat([self.pconv(x).flatten(1), clock], dim=1))
+        value = self.vlinear(torch.cat([self.vconv(x).flatten(1), clock], dim=1))
+        return logits, value
 
     @classmethod
     def process_observation(cls, observation):

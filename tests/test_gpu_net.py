@@ -23,10 +23,10 @@ def _softmax(x):
     return e / e.sum()
 
 
-# f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 64, 128);
+# f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 8, 128);
 # f16x3-x* = k_net_x (32x32x16 MFMA, variant bit 512) and its schedules; fp32 = fp32 MFMA path
 NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4), 'f16x3-y128': ('f16x3', 128),
-               'f16x3-y64': ('f16x3', 64), 'f16x3-x': ('f16x3', 512)}
+               'f16x3-y8': ('f16x3', 8), 'f16x3-x': ('f16x3', 512)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
@@ -101,6 +101,70 @@ def test_mix_epilogue_bit_identical():
     torch.manual_seed(0)
     eng.set_weights(Network())
     pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=5)])
+    eng.set_net_variant(0)
+    l0, v0 = eng.evaluate(pos)
+    eng.set_net_variant(1024)
+    l1, v1 = eng.evaluate(pos)
+    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
+def _wide_range_net(gain=6.0):
+    """Random-init net whose residual blocks amplify: both BatchNorm gammas of every block x
+    `gain`, so the trunk's activations reach ~7e6 (f16's max is 65504)."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    with torch.no_grad():
+        for blk in list(net.resbody)[1:]:
+            blk.convblock1.layers[1].weight.mul_(gain)
+            blk.convblock2.layers[1].weight.mul_(gain)
+    return net.eval()
+
+
+def test_dynamic_range_beyond_f16():
+    """k_net_y keeps fp32's range (a per-workgroup power-of-two image scale chosen from a weight
+    bound).  With trunk activations ~7e6 the logits match torch's fp32 eval forward to 1e-5 of
+    each row's largest logit (the fp32 error scale at these magnitudes), values (saturated tanh)
+    to 1e-5, and the best legal move agrees wherever its margin exceeds that error scale."""
+    import torch
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen, pos_legal
+    from minitchess_alphazero_amd.learner import collate_fn
+    from tests_positions import random_fens
+    net = _wide_range_net()
+    fens = random_fens(129, seed=9)
+    eng = Engine(n_games=64, sims=4)
+    eng.set_weights(net)
+    pos = np.stack([pos_from_fen(f) for f in fens])
+    logits, values = eng.evaluate(pos)
+    rows = [{'observation': f, 'legal_moves': [], 'pi': [], 'reward': 0.0} for f in fens]
+    _, tok, clk, _ = collate_fn(rows)
+    with torch.no_grad():
+        p, v = net.cuda()((tok.cuda(), clk.cuda()))
+    p, v = p.double().cpu().numpy(), v[:, 0].double().cpu().numpy()
+    assert np.abs(p).max() > 1e5                          # the trunk really left f16's range
+    scale = np.abs(p).max(axis=1, keepdims=True)
+    assert np.max(np.abs(logits - p) / scale) <= 1e-5
+    assert np.max(np.abs(values - v)) <= 1e-5
+    for i in range(len(fens)):
+        legal = pos_legal(pos[i])
+        if len(set(legal)) > 1:
+            ref = np.sort(p[i][legal])
+            if ref[-1] - ref[-2] > 1e-4 * scale[i, 0]:
+                assert legal[int(np.argmax(logits[i][legal]))] == legal[int(np.argmax(p[i][legal]))]
+
+
+def test_dynamic_range_epilogue_bit_identical():
+    """With the image scale active (xs > 0), the v_fma_mix epilogue still stores exactly the
+    bits of the unfused form (variant 1024)."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from tests_positions import random_fens
+    eng = Engine(n_games=64, sims=4)
+    eng.set_weights(_wide_range_net())
+    pos = np.stack([pos_from_fen(f) for f in random_fens(97, seed=4)])
     eng.set_net_variant(0)
     l0, v0 = eng.evaluate(pos)
     eng.set_net_variant(1024)

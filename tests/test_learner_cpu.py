@@ -1,0 +1,130 @@
+"""CPU: learner vs the reference's own collate/loss/gradients
+(tests/golden/learner.*, recorded by make_golden_learner.py), and the product learner vs the
+oracle restatement (oracle/learner.py) on a full seeded update."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+META = json.load(open(os.path.join(GOLDEN, 'learner.json')))
+Z = np.load(os.path.join(GOLDEN, 'learner.npz'))
+
+
+def _check_collate(out):
+    pib, ch, clk, rew = out
+    assert pib.dtype == torch.float32 and ch.dtype == torch.int64
+    assert tuple(ch.shape) == (32, 2, 6, 5) and tuple(clk.shape) == (32, 1) and tuple(rew.shape) == (32, 1)
+    assert np.array_equal(pib.numpy(), Z['pib'])
+    assert np.array_equal(ch.numpy(), Z['channels'].astype(np.int64))
+    assert np.array_equal(clk.numpy(), Z['clock'])
+    assert np.array_equal(rew.numpy(), Z['reward'])
+
+
+def test_oracle_collate_matches_reference():
+    from oracle.learner import collate_fn
+    assert META['rows_with_repeated_codes'] > 0
+    _check_collate(collate_fn(META['batch']))
+
+
+def test_product_collate_matches_reference():
+    from minitchess_alphazero_amd.learner import collate_fn
+    _check_collate(collate_fn(META['batch']))
+
+
+def test_avg_smooth_loss_matches_reference():
+    from minitchess_alphazero_amd.learner import AvgSmoothLoss
+    m = AvgSmoothLoss().reset()
+    vals = []
+    for x in META['avg_smooth_inputs']:
+        m.accumulate(x)
+        vals.append(m.value)
+    assert vals == META['avg_smooth_values']
+
+
+def test_training_forward_loss_grads_match_reference():
+    """Train-mode forward + loss + backward of the product Network on CPU vs the reference."""
+    from minitchess_alphazero_amd.learner import collate_fn
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network().train()
+    pib, ch, clk, rew = collate_fn(META['batch'])
+    p, v = net((ch, clk))                      # one train-mode forward (updates BN running stats once)
+    assert np.allclose(p.detach().numpy(), Z['logits'], rtol=0, atol=1e-5)
+    assert np.allclose(v.detach().numpy(), Z['values'], rtol=0, atol=1e-6)
+    loss = ((v - rew) ** 2 - (pib * p.log_softmax(-1)).sum(1)).mean()    # exp/learner.py:86-87
+    assert abs(float(loss) - META['loss']) <= 1e-5 * abs(META['loss'])
+    loss.backward()
+    named = dict(net.named_parameters())
+    for k, ref in META['grad_norms'].items():
+        got = float(named[k].grad.double().norm())
+        assert abs(got - ref) <= 1e-4 * ref + 1e-9, k
+    for k in META['small_grads']:
+        assert np.allclose(named[k].grad.numpy(), Z['grad/' + k], rtol=1e-4, atol=1e-7), k
+    sd = net.state_dict()
+    for key in Z.files:
+        if key.startswith('running/'):
+            assert np.allclose(sd[key[8:]].numpy(), Z[key], rtol=1e-5, atol=1e-7), key
+
+
+def test_sampler_order_equals_dataloader_order():
+    from minitchess_alphazero_amd.learner import sampler_order
+    rows = list(range(77))
+    torch.manual_seed(123)
+    ref = [i for b in torch.utils.data.DataLoader(rows, batch_size=8, shuffle=True) for i in b.tolist()]
+    torch.manual_seed(123)
+    assert sampler_order(77) == ref
+
+
+def _rows(n_games=2):
+    t = json.load(open(os.path.join(GOLDEN, 'trees.json')))
+    return [{k: m[k] for k in ('observation', 'legal_moves', 'pi', 'reward')}
+            for g in t['synthetic'][:n_games] for m in g['moves']]
+
+
+@pytest.mark.slow
+def test_learner_update_equals_oracle_update_cpu():
+    """A full seeded update (fresh AdamW lr 0.2, batch 32, shuffled) on CPU: the product
+    learner (resident batches) and the oracle (DataLoader + collate_fn) take the same batches
+    in the same order and end with the same parameters."""
+    import oracle.learner as ol
+    from minitchess_alphazero_amd.learner import SimpleAlphaZeroDataset, SimpleAlphaZeroLearner
+    from minitchess_alphazero_amd.network import Network
+    from oracle.net import Network as ONet
+    rows = _rows(2)[:70]
+    torch.manual_seed(0)
+    a = Network()
+    torch.manual_seed(0)
+    b = ONet()
+    ds = SimpleAlphaZeroDataset(1000)
+    ds.push(rows)
+    lrn = SimpleAlphaZeroLearner(None, 36, a, batch_size=32, epochs=1, optim_params={'lr': 0.2}, device='cpu')
+    torch.manual_seed(7)
+    lrn.update(ds)
+    ods = ol.Dataset(1000)
+    ods.push(rows)
+    torch.manual_seed(7)
+    trace = ol.update(b, ods, 32, 1, {'lr': 0.2})
+    assert len(lrn.last_losses) == len(trace) == 3
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa:
+        assert torch.allclose(sa[k].float(), sb[k].float(), rtol=1e-5, atol=1e-6), k
+
+
+def test_learn_puppet_state_machine():
+    from minitchess_alphazero_amd.learner import LearnPuppet
+    lp = LearnPuppet('u', batch_size=32, epochs=1, optim_params={'lr': 0.2}, device='cpu')
+    v0 = lp.weights_version
+    rows = _rows(1)[:10]
+    lp.push_data(rows)
+    assert lp.episode_counter == 1 and len(lp._dataset) == 10
+    lp.train()
+    lp.push_data(rows)                      # ignored while training (app/base.py:182-185)
+    assert lp.episode_counter == 1 and len(lp._dataset) == 10
+    assert lp.status == 'TRAIN'
+    lp.simulate()
+    assert lp.status == 'SIMULATE'
+    assert lp.weights_version == v0 and set(lp.get_weights_dict()) == {'weights', 'version'}
