@@ -95,15 +95,20 @@ class ResidentBatches:
 
     def __init__(self, rows, device):
         self.device = torch.device(device)
-        pos = np.stack([pos_from_fen(r['observation']) for r in rows]) if rows else np.zeros((0, 5), np.uint32)
+        if isinstance(rows, EpisodeRecords):
+            pos, pi, reward = rows.pos, rows.pi_dense(), rows.reward
+        else:
+            pos = np.stack([pos_from_fen(r['observation']) for r in rows]) if rows else np.zeros((0, 5), np.uint32)
+            pi = dense_pi(rows)
+            reward = np.asarray([float(r['reward']) for r in rows], np.float32)
         if self.device.type == 'cuda':
             self.tokens, self.clock = encode_positions(pos, self.device)
         else:   # host encoder (CPU tests; the product learner runs on the GPU)
             enc = [pos_encode(p) for p in pos]
             self.tokens = torch.from_numpy(np.stack([t for t, _ in enc])).reshape(-1, 2, 6, 5)
             self.clock = torch.tensor(np.asarray([c for _, c in enc], np.float32)).reshape(-1, 1)
-        self.pi = torch.from_numpy(dense_pi(rows)).to(self.device)
-        self.reward = torch.tensor(np.asarray([float(r['reward']) for r in rows], np.float32)).reshape(-1, 1).to(self.device)
+        self.pi = torch.from_numpy(pi).to(self.device)
+        self.reward = torch.from_numpy(np.ascontiguousarray(reward, np.float32)).reshape(-1, 1).to(self.device)
 
     def __len__(self):
         return self.pi.shape[0]
@@ -111,6 +116,69 @@ class ResidentBatches:
     def batch(self, idx):
         i = torch.as_tensor(idx, dtype=torch.long, device=self.device)
         return self.pi[i], self.tokens[i], self.clock[i], self.reward[i]
+
+
+class EpisodeRecords:
+    """Self-play rows as packed arrays in Engine.records() layout: pos [N,5] u32, k [N] legal
+    list lengths, codes / visits concatenated over rows, reward [N].  pi = visits / sum(visits)
+    per row (float64, as Engine.episodes / exp/policy.py:120 compute it).  The loop moves these
+    arrays between ranks instead of FEN-keyed dicts."""
+
+    def __init__(self, pos, k, codes, visits, reward):
+        self.pos = np.ascontiguousarray(pos, np.uint32).reshape(-1, 5)
+        self.k = np.ascontiguousarray(k, np.int32)
+        self.codes = np.ascontiguousarray(codes, np.uint16)
+        self.visits = np.ascontiguousarray(visits, np.uint32)
+        self.reward = np.ascontiguousarray(reward, np.float32)
+
+    @classmethod
+    def from_engine(cls, rec):
+        return cls(rec['pos'], rec['k'], rec['codes'], rec['visits'], rec['reward'])
+
+    @classmethod
+    def concat(cls, parts):
+        parts = [p for p in parts if len(p)]
+        if not parts:
+            return cls(np.zeros((0, 5), np.uint32), [], [], [], [])
+        return cls(np.concatenate([p.pos for p in parts]), np.concatenate([p.k for p in parts]),
+                   np.concatenate([p.codes for p in parts]), np.concatenate([p.visits for p in parts]),
+                   np.concatenate([p.reward for p in parts]))
+
+    def __len__(self):
+        return int(self.k.shape[0])
+
+    def tail(self, n):
+        """The last n rows (deque(maxlen) semantics of exp/dataset.py:8)."""
+        if n >= len(self):
+            return self
+        start = len(self) - n
+        e0 = int(self.k[:start].sum())
+        return EpisodeRecords(self.pos[start:], self.k[start:], self.codes[e0:], self.visits[e0:], self.reward[start:])
+
+    def pi_dense(self):
+        """[N, 554] float32 targets, the same values and duplicate rule as dense_pi(rows)."""
+        n = len(self)
+        out = np.zeros((n, NUM_ACTIONS), np.float32)
+        if n == 0:
+            return out
+        row = np.repeat(np.arange(n), self.k)
+        starts = np.concatenate([[0], np.cumsum(self.k)[:-1]])
+        sums = np.add.reduceat(self.visits.astype(np.float64), starts)
+        vals = (self.visits.astype(np.float64) / sums[row]).astype(np.float32)
+        out[row, self.codes.astype(np.int64)] = vals   # repeated (row, code): the last occurrence is kept
+        return out
+
+    def to_rows(self):
+        """dict rows (exp/callbacks.py:40-47 InfoRecorder format, without 'action')."""
+        from .environment import pos_to_fen
+        rows, e = [], 0
+        for i in range(len(self)):
+            k = int(self.k[i])
+            N = self.visits[e:e + k].astype(np.float64)
+            rows.append({'observation': pos_to_fen(self.pos[i]), 'legal_moves': [int(c) for c in self.codes[e:e + k]],
+                         'pi': (N / N.sum()).tolist(), 'reward': float(self.reward[i])})
+            e += k
+        return rows
 
 
 def sampler_order(n):
@@ -161,28 +229,93 @@ class SimpleAlphaZeroLearner:
         self.last_losses = []
 
     def update(self, dataset):
-        """One learner update over `dataset` (rows or SimpleAlphaZeroDataset).  Returns the
-        smoothed loss; per-batch values in self.last_losses."""
-        rows = dataset.get_memory() if hasattr(dataset, 'get_memory') else list(dataset)
+        """One learner update over `dataset` (rows, SimpleAlphaZeroDataset or EpisodeRecords).
+        Returns the smoothed loss; per-batch values in self.last_losses.
+
+        On a GPU the full-size batch step (gather, forward, loss, backward, AdamW) is captured
+        once per update in a HIP graph and replayed per batch: at the reference's batch of 32
+        the step is launch-bound.  The graph is captured after warm-up steps, and the weights,
+        BatchNorm buffers and optimizer state are then restored to their pre-warm-up values,
+        so the replayed steps are the reference's steps; AdamW runs with capturable=True (its
+        step count on the device).  A partial last batch runs eagerly."""
+        if isinstance(dataset, EpisodeRecords):
+            rows = dataset
+        else:
+            rows = dataset.get_memory() if hasattr(dataset, 'get_memory') else list(dataset)
         model = self._network.train().to(self._device)
-        optimizer = torch.optim.AdamW(model.parameters(), **self._optim_params)
         data = ResidentBatches(rows, self._device)
+        use_graph = self.graphs and self._device.type == 'cuda' and len(data) >= self._batch_size
+        optimizer = torch.optim.AdamW(model.parameters(), **self._optim_params,
+                                      **({'capturable': True} if use_graph else {}))
+        step = self._graph_step(model, optimizer, data) if use_graph else None
         metric = AvgSmoothLoss().reset()
         losses = []
         for epoch in range(self._epochs):
             order = sampler_order(len(data))
+            pending = []
             for s in range(0, len(order), self._batch_size):
-                pib, tok, clk, rew = data.batch(order[s:s + self._batch_size])
+                idx = order[s:s + self._batch_size]
+                if step is not None and len(idx) == self._batch_size:
+                    pending.append(step(idx))
+                    continue
+                pib, tok, clk, rew = data.batch(idx)
                 loss = alphazero_loss(model, pib, tok, clk, rew)
                 optimizer.zero_grad()
                 loss.backward()
-                lv = float(loss.detach().item())
-                metric.accumulate(lv)
-                losses.append(lv)
+                pending.append(loss.detach().clone())
                 optimizer.step()
+            for lt in torch.stack(pending).tolist() if pending else []:   # one sync per epoch
+                metric.accumulate(lt)
+                losses.append(lt)
             log.info('Epoch %d: %.2f', epoch, metric.value if metric.count else float('nan'))
         self.last_losses = losses
         return metric.value if metric.count else float('nan')
+
+    graphs = True
+
+    def _graph_step(self, model, optimizer, data):
+        """Capture one full-batch training step; returns step(idx) -> loss tensor (a copy)."""
+        dev = self._device
+        static_idx = torch.zeros(self._batch_size, dtype=torch.long, device=dev)
+        static_loss = torch.zeros((), dtype=torch.float32, device=dev)
+        saved = {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+        def body():
+            pib, tok, clk, rew = data.pi[static_idx], data.tokens[static_idx], data.clock[static_idx], \
+                data.reward[static_idx]
+            loss = alphazero_loss(model, pib, tok, clk, rew)
+            optimizer.zero_grad(set_to_none=False)
+            loss.backward()
+            optimizer.step()
+            static_loss.copy_(loss.detach())
+
+        static_idx.copy_(torch.arange(self._batch_size, device=dev) % len(data))
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            body()
+        # undo the warm-up and capture steps: weights, BN buffers, AdamW moments and step count
+        with torch.no_grad():
+            for k, v in model.state_dict().items():
+                v.copy_(saved[k])
+            for st in optimizer.state.values():
+                for t in st.values():
+                    if torch.is_tensor(t):
+                        t.zero_()
+            for p in model.parameters():
+                if p.grad is not None:
+                    p.grad.zero_()
+
+        def step(idx):
+            static_idx.copy_(torch.as_tensor(idx, dtype=torch.long).to(dev, non_blocking=True))
+            graph.replay()
+            return static_loss.clone()
+        return step
 
 
 # ---- LearnPuppet (app/base.py:137-205, transport excluded) --------------------------------------------
@@ -202,6 +335,7 @@ class LearnPuppet:
 
     def _init_dataset(self):
         self._dataset = SimpleAlphaZeroDataset(max_length=self._max_length)
+        self._records = EpisodeRecords.concat([])
 
     @property
     def episode_counter(self):
@@ -236,11 +370,18 @@ class LearnPuppet:
             self._episode_counter += 1
             self._dataset.push(data)
 
+    def push_records(self, records, episodes):
+        """push_data for packed rows (EpisodeRecords) of `episodes` episodes."""
+        if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
+            self._episode_counter += episodes
+            self._records = EpisodeRecords.concat([self._records, records]).tail(self._max_length)
+
     def update(self):
         """app/base.py:188-195: load the current weights, train on the dataset, publish the new
         weights as a new version, start a fresh dataset."""
         self._network.load_state_dict(self.weights)
-        loss = self._learner.update(self._dataset)
+        data = self._records if len(self._records) else self._dataset
+        loss = self._learner.update(data)
         self.weights = self._network.state_dict()
         self._init_dataset()
         out = self.get_weights_dict()

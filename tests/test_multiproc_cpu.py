@@ -65,3 +65,58 @@ def test_shard_bounds():
     assert shard(3, 8, 4096) == (3 * 4096, 4096)
     with pytest.raises(ValueError):
         shard(8, 8, 4096)
+
+
+def _loop_worker(rank, world, port, q):
+    """The C5 exchange of minitchess_alphazero_amd.loop over gloo: each rank's records reach
+    rank 0 in rank order; rank 0 trains (CPU learner) and its new weights reach every rank."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from minitchess_alphazero_amd.learner import EpisodeRecords, SimpleAlphaZeroLearner
+    from minitchess_alphazero_amd.loop import broadcast_weights, flat_weights, gather_records
+    from minitchess_alphazero_amd.network import Network
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    rng = np.random.RandomState(rank)
+    n = 3 + rank
+    k = rng.randint(1, 6, size=n)
+    rec = EpisodeRecords(np.tile(np.array([[0x00000000, 0, 0, 0, 1 | (1 << 16)]], np.uint32), (n, 1)), k,
+                         rng.randint(0, 554, size=k.sum()), rng.randint(1, 9, size=k.sum()), rng.choice([-1., 0., 1.], n))
+    parts = gather_records(rec, dist)
+    torch.manual_seed(100 + rank)                  # ranks start from different weights
+    net = Network()
+    if rank == 0:
+        from minitchess_alphazero_amd.environment import STARTING_FEN, pos_from_fen
+        allrec = EpisodeRecords.concat(parts)
+        allrec.pos[:] = pos_from_fen(STARTING_FEN)
+        SimpleAlphaZeroLearner(None, 36, net, 4, 1, {'lr': 0.01}, device='cpu').update(allrec)
+    broadcast_weights(net, dist, 'cpu')
+    flat, _ = flat_weights(net, 'cpu')
+    q.put((rank, parts and [(p.k.tolist(), p.codes.tolist(), p.visits.tolist(), p.reward.tolist()) for p in parts],
+           rec.k.tolist(), rec.codes.tolist(), flat.double().sum().item(), flat[:1000].tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_loop_exchange_two_ranks():
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loop_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=300)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    parts = res[0][1]
+    assert [p[0] for p in parts] == [res[0][2], res[1][2]]          # rank order, intact
+    assert [p[1] for p in parts] == [res[0][3], res[1][3]]
+    assert res[1][1] is None
+    assert res[0][4] == res[1][4] and res[0][5] == res[1][5]           # identical weights after broadcast
