@@ -121,6 +121,12 @@ int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int s
                   uint64_t* stamps_out);
 /* select a network kernel code variant for A/B timing (0 = the product kernel k_net_y) */
 int mtaz_set_net_variant(mtaz_engine* h, int variant);
+/* Two-network play (the arena of exp/learner.py:97-145): upload a network into weight slot 0
+ * or 1 (mtaz_set_weights fills slot 0), and map agent 0 (the first mover, exp/agent.py:11-14)
+ * and agent 1 to slots.  With different slots, mtaz_play evaluates each move's leaves with the
+ * network of the agent to move (games from STARTING_FEN move in lockstep). */
+int mtaz_set_weights_slot(mtaz_engine* h, int slot, const float* const* d_tensors, const int64_t* numels, int n);
+int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_agent1);
 /* mtaz_play over `groups` independent game groups (1 = off; must divide n_games): each group
  * has its own HIP stream and host thread, so one group's tree kernels and network tail run
  * while another's network occupies the GPU.  Games keep their global seeds, so results are

@@ -53,6 +53,8 @@ SIGNATURES = {
     'mtaz_set_seed_base': (c_int, [c_void_p, c_uint64]),
     'mtaz_set_net_variant': (c_int, [c_void_p, c_int]),
     'mtaz_set_pipeline': (c_int, [c_void_p, c_int]),
+    'mtaz_set_weights_slot': (c_int, [c_void_p, c_int, POINTER(c_void_p), P_i64, c_int]),
+    'mtaz_set_agent_slots': (c_int, [c_void_p, c_int, c_int]),
     'mtaz_net_time': (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, P_f32, POINTER(c_uint64)]),
     'mtaz_set_games': (c_int, [c_void_p, P_u32, P_i32, P_u8, c_int]),
     'mtaz_get_games': (c_int, [c_void_p, P_u32, P_i32, P_u8, P_i32]),

@@ -494,6 +494,19 @@ struct mtaz_engine {
   int wave = 0;
   int groups = 1;                       // mtaz_set_pipeline
   std::vector<mtaz_engine*> parts;      // per-group engines (borrow this engine's weights)
+  // two-network play (arena, exp/learner.py:97-145): weight slot 0 / 1; the active slot's
+  // buffers are the fields above (w, wbuf, wxbuf, wxinv, wyrange, weights_ok), the other
+  // slot's are parked here; agent_slot maps agent 0 (first mover) / agent 1 to a slot
+  struct Parked {
+    NetWeights w{};
+    float* wbuf = nullptr;
+    uint4* wxbuf = nullptr;
+    float* wxinv = nullptr;
+    float* wyrange = nullptr;
+    bool ok = false;
+  } parked;
+  int cur_slot = 0;
+  int agent_slot[2] = {0, 0};
 
   ~mtaz_engine() {
     for (mtaz_engine* p : parts) delete p;
@@ -945,6 +958,37 @@ extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   return 0;
 }
 
+static void swap_slot(mtaz_engine* h) {
+  std::swap(h->w, h->parked.w);
+  std::swap(h->wbuf, h->parked.wbuf);
+  std::swap(h->wxbuf, h->parked.wxbuf);
+  std::swap(h->wxinv, h->parked.wxinv);
+  std::swap(h->wyrange, h->parked.wyrange);
+  std::swap(h->weights_ok, h->parked.ok);
+  h->cur_slot ^= 1;
+}
+
+static void activate_slot(mtaz_engine* h, int slot) {
+  if (slot != h->cur_slot) swap_slot(h);
+}
+
+extern "C" int mtaz_set_weights_slot(mtaz_engine* h, int slot, const float* const* d_tensors, const int64_t* numels,
+                                     int n) {
+  if (slot != 0 && slot != 1) return set_err(MTAZ_E_FAIL, "weight slot must be 0 or 1");
+  const int cur = h->cur_slot;
+  activate_slot(h, slot);
+  const int rc = mtaz_set_weights(h, d_tensors, numels, n);
+  activate_slot(h, cur);
+  return rc;
+}
+
+extern "C" int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_agent1) {
+  if ((slot_agent0 | slot_agent1) & ~1) return set_err(MTAZ_E_FAIL, "weight slots must be 0 or 1");
+  h->agent_slot[0] = slot_agent0;
+  h->agent_slot[1] = slot_agent1;
+  return 0;
+}
+
 extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
   if (groups < 1 || h->G % groups != 0) return set_err(MTAZ_E_FAIL, "groups=%d must divide n_games=%d", groups, h->G);
   if (groups != h->groups) {
@@ -1240,7 +1284,17 @@ static int play_groups(mtaz_engine* h) {
 extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
   if (n_games > h->G || n_games <= 0) return set_err(MTAZ_E_CAPACITY, "n_games=%d (engine has %d)", n_games, h->G);
-  if (h->groups > 1 && !from_current && n_games == h->G) return play_groups(h);
+  const bool two_nets = h->agent_slot[0] != h->agent_slot[1];
+  if (two_nets) {
+    for (int a = 0; a < 2; ++a) {
+      activate_slot(h, h->agent_slot[a]);
+      if (!h->weights_ok) {
+        activate_slot(h, 0);
+        return set_err(MTAZ_E_FAIL, "two-network play: weight slot %d is empty", h->agent_slot[a]);
+      }
+    }
+  }
+  if (h->groups > 1 && !two_nets && !from_current && n_games == h->G) return play_groups(h);
   HIPCHK(hipSetDevice(h->device));
   const double t0 = now_ms();
   const int G = h->G;
@@ -1277,6 +1331,15 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     int n_active = 0;
     for (int g = 0; g < G; ++g) n_active += active[g];
     if (!n_active) break;
+    if (two_nets) {   // lockstep games: every active game has the same agent to move
+      int a = -1;
+      for (int g = 0; g < G; ++g)
+        if (active[g]) {
+          if (a >= 0 && agents[g] != a) return set_err(MTAZ_E_FAIL, "two-network play needs games in lockstep");
+          a = agents[g];
+        }
+      activate_slot(h, h->agent_slot[a]);
+    }
     double ts = now_ms();
     ECHK(mtaz_move_begin(h, root_k.data(), root_new.data()));
     sync_ms += now_ms() - ts;
@@ -1339,6 +1402,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     h->stats[ST_SIMS] += (double)n_active * h->sims;
     ++moves;
   }
+  if (two_nets) activate_slot(h, 0);
   for (int g = 0; g < G; ++g) h->final_outcome[g] = outcome_v[g];
   // stats
   std::vector<int32_t> counts(std::min(h->wave, h->count_log_cap));

@@ -62,8 +62,9 @@ class Engine:
             pass
 
     # ---- weights / evaluation ---------------------------------------------------------------
-    def set_weights(self, network_or_state_dict):
-        """SimulatePuppet.load_weights (app/base.py:126-129); BN folded on upload."""
+    def set_weights(self, network_or_state_dict, slot=0):
+        """SimulatePuppet.load_weights (app/base.py:126-129); BN folded on upload.  slot 1 holds
+        a second network for two-network play (set_agent_networks)."""
         import torch
         from .network import weight_tensors
         dev = torch.device('cuda', self.device)
@@ -71,7 +72,11 @@ class Engine:
         torch.cuda.synchronize(dev)
         ptrs = (c_void_p * len(ts))(*[t.data_ptr() for t in ts])
         numels = np.array([t.numel() for t in ts], np.int64)
-        _lib.check(self.L.mtaz_set_weights(self.h, ptrs, _p(numels, c_int64), len(ts)))
+        _lib.check(self.L.mtaz_set_weights_slot(self.h, int(slot), ptrs, _p(numels, c_int64), len(ts)))
+
+    def set_agent_networks(self, slot_agent0=0, slot_agent1=0):
+        """Which weight slot agent 0 (moves first) and agent 1 search with; (0, 0) = self-play."""
+        _lib.check(self.L.mtaz_set_agent_slots(self.h, int(slot_agent0), int(slot_agent1)))
 
     def evaluate(self, positions):
         """Network.forward on packed positions [n,5] -> (logits [n,554], values [n]) (numpy)."""

@@ -14,7 +14,11 @@ torch.distributed, with no transport layer between the steps:
      on PyTorch-ROCm);
   4. the new weights (the 133 float tensors the engine consumes, 42.8 MB) are broadcast from
      rank 0 as ONE flat float32 buffer (RCCL over xGMI with the nccl backend) and
-     every rank uploads them into its engine.
+     every rank uploads them into its engine;
+  5. optional gating (--arena-games > 0; the reference's arena and 0.55 gate are commented
+     out, exp/learner.py:97-145, app/base.py:194-196, so the default keeps every update):
+     every rank plays its shard of arena games new-vs-previous (minitchess_alphazero_amd.arena),
+     the win counts are all-reduced, and all ranks keep or revert the weights alike.
 Run: python -m minitchess_alphazero_amd.loop [--iterations I --games G --sims S]
      N GPUs: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 -m ...
 """
@@ -69,8 +73,23 @@ def gather_records(rec, dist, dst=0):
     return [EpisodeRecords(o['pos'], o['k'], o['codes'], o['visits'], o['reward']) for o in out]
 
 
+def arena_round(new_net, old_net, games, sims, dist, device, seed_base):
+    """Sharded arena: each rank plays `games` games per side; counts summed over ranks."""
+    from .arena import arena
+    from .engine import Engine
+    eng = Engine(n_games=games, sims=sims, device=device)
+    res = arena(eng, new_net, old_net, seed_base=seed_base)
+    cnt = torch.tensor([res['new_wins'], res['old_wins'], res['draws'], res['games']], dtype=torch.float64,
+                       device=torch.device('cuda', device))
+    if dist is not None:
+        dist.all_reduce(cnt)
+    nw, ow, dr, ng = cnt.tolist()
+    return {'new_wins': int(nw), 'old_wins': int(ow), 'draws': int(dr), 'games': int(ng),
+            'score': nw / (nw + ow + 1e-8)}
+
+
 def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None, device=0, seed=0,
-             log=print):
+             log=print, arena_games=0, gate_threshold=0.55):
     """C5 on this node.  Returns rank 0's per-iteration history (other ranks: [])."""
     from .engine import Engine
     rank = dist.get_rank() if dist is not None else 0
@@ -95,7 +114,9 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
         parts = gather_records(rec, dist)
         t2 = time.perf_counter()
         out = None
+        old_sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
         if rank == 0:
+            old_version = learner.weights_version
             learner.push_records(EpisodeRecords.concat(parts), games * world)
             learner.train()
             out = learner.update()
@@ -104,6 +125,18 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
         torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
         broadcast_weights(net, dist, dev)
+        verdict = None
+        if arena_games > 0:
+            prev = Network()
+            prev.load_state_dict(old_sd)
+            verdict = arena_round(net, prev, arena_games, sims, dist, device,
+                                  seed_base=10 ** 9 + (it * world + rank) * 2 * arena_games)
+            verdict['accepted'] = verdict['score'] > gate_threshold
+            if not verdict['accepted']:
+                net.load_state_dict(old_sd)
+                if rank == 0:
+                    learner._weights = {k: v.detach().cpu().clone() for k, v in old_sd.items()}
+                    learner._weights_version = old_version
         eng.set_weights(net)
         torch.cuda.synchronize(dev)
         t4 = time.perf_counter()
@@ -114,6 +147,8 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
                  'train_s': t3 - t2, 'broadcast_s': t4 - t3, 'iteration_s': t4 - t0,
                  'games_per_s': games * world / (t4 - t0), 'samples_per_s_train': rows / (t3 - t2),
                  'plies_per_game': st['plies'] / games}
+            if verdict is not None:
+                h['arena'] = verdict
             history.append(h)
             log(json.dumps(h))
     return history, net
@@ -128,6 +163,8 @@ def main(argv=None):
     ap.add_argument('--epochs', type=int, default=1)
     ap.add_argument('--lr', type=float, default=0.2)
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--arena-games', type=int, default=0, help='arena games per side per GPU (0: no gating)')
+    ap.add_argument('--gate', type=float, default=0.55)
     ap.add_argument('--save', default='', help='write the final state_dict here (torch.save)')
     args = ap.parse_args(argv)
     world = int(os.environ.get('WORLD_SIZE', 1))
@@ -139,7 +176,7 @@ def main(argv=None):
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     hist, net = run_loop(args.iterations, args.games, args.sims, args.batch, args.epochs, args.lr, dist, local,
-                         args.seed)
+                         args.seed, arena_games=args.arena_games, gate_threshold=args.gate)
     if (dist is None or dist.get_rank() == 0) and args.save:
         torch.save(net.state_dict(), args.save)
     if dist is not None:

@@ -122,3 +122,13 @@ def test_host_rng_long_streams_vs_numpy():
             out = np.zeros(5, np.float64)
             L.mtaz_rng_dirichlet(st, alpha, 5, _lib.ptr(out, ctypes.c_double))
             assert np.array_equal(out, ref), (seed, alpha)
+
+
+def test_arena_winner_rule_cpu():
+    """WinnerRecorder (exp/callbacks.py:19-22): the agent that made the last move of a decisive
+    game wins; agent 0 moves first; draws are not counted."""
+    import numpy as np
+    from minitchess_alphazero_amd.arena import gate, winners
+    rec = {'plies': np.array([1, 2, 7, 10, 5]), 'outcome': np.array([1, 1, 1, 2, 1])}
+    assert winners(rec) == {False: 3, True: 1}
+    assert gate(0.56) and not gate(0.55)
