@@ -167,16 +167,16 @@ def test_loop_two_iterations_single_gpu():
 
 def test_graph_captured_update_equals_eager_update():
     """The HIP-graph learner step (capturable AdamW, warm-up undone) takes the same steps as the
-    eager loop: exactly one AdamW step per batch and the same loss trace (the first loss, before
-    any step, to 1e-6; later ones to 1e-4).  lr 1e-3 here: at the reference's lr 0.2 the first
-    AdamW steps (+-0.2 per weight on a random-init net) are chaotic, and capturable AdamW's
-    device-side bias correction (fp32) vs the eager one (host double) already moves later losses
-    by ~0.2%."""
+    eager loop (lr 1e-3, where AdamW is smooth):
+      * exactly one AdamW step per batch, and every weight within 1e-4 of the eager run (warm-up
+        or capture steps left in place would move weights by >= 3 AdamW steps, ~3e-3);
+      * the same loss trace: the first loss (before any step) to 1e-6, later ones to 1e-3 (GPU
+        backward reductions are not bitwise deterministic run to run)."""
     import torch
     from minitchess_alphazero_amd.learner import SimpleAlphaZeroLearner
     from minitchess_alphazero_amd.network import Network
     rows = _rows(3)[:150]
-    traces = []
+    traces, weights = [], []
     for graphs in (False, True):
         torch.manual_seed(0)
         net = Network()
@@ -197,10 +197,12 @@ def test_graph_captured_update_equals_eager_update():
         steps = {float(st['step']) for st in seen['opt'].state.values()}
         assert steps == {5.0}, steps                   # 4 graph replays + 1 eager tail batch
         traces.append(np.array(lrn.last_losses))
+        weights.append({k: v.detach().float().cpu() for k, v in net.named_parameters()})
     l0, l1 = traces
     assert len(l0) == len(l1) == 5
     assert abs(l0[0] - l1[0]) <= 1e-6 * abs(l0[0])
-    assert np.allclose(l0, l1, rtol=1e-4)
+    assert np.allclose(l0, l1, rtol=1e-3)
+    assert max(float((weights[0][k] - weights[1][k]).abs().max()) for k in weights[0]) <= 1e-4
 
 
 def test_loop_with_arena_gate():
