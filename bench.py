@@ -57,6 +57,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
+    ap.add_argument('--weights', default='', help='state_dict file (torch.save) instead of random init '
+                                                  '(BASELINE config 3: a checkpoint trained by the loop)')
     args = ap.parse_args()
 
     import numpy as np
@@ -84,8 +86,21 @@ def main():
     G, sims = args.games, args.sims
     seed_base, _ = shard(rank, world, G)
     eng = Engine(n_games=G, sims=sims, device=device, seed_base=seed_base)
-    torch.manual_seed(0)                      # random-init weights of the reference architecture
-    eng.set_weights(Network())
+    weights_sha = None
+    if args.weights:
+        import hashlib
+        sd = torch.load(args.weights, map_location='cpu', weights_only=True)
+        h = hashlib.sha256()
+        for k, v in sd.items():
+            h.update(k.encode())
+            h.update(v.detach().cpu().contiguous().numpy().tobytes())
+        weights_sha = h.hexdigest()
+        net = Network()
+        net.load_state_dict(sd)
+        eng.set_weights(net)
+    else:
+        torch.manual_seed(0)                      # random-init weights of the reference architecture
+        eng.set_weights(Network())
     eng.set_precision(args.precision)
     eng.set_timing(True)
     eng.set_pipeline(args.groups)
@@ -152,9 +167,12 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'f16x3 (fp16 hi/lo split, fp32 accumulate; fp32-accurate)' if f16x3 else 'fp32',
-        'data': 'synthetic: self-play from STARTING_FEN, random-init weights (torch.manual_seed(0); Network())',
-        'config': {'workload': f'{G} parallel self-play games per GPU, {sims} sims/move, random-init policy net '
-                               f'(BASELINE config 2; config 4 = 8 GPUs x 4096)',
+        'data': ('synthetic: self-play from STARTING_FEN, random-init weights (torch.manual_seed(0); Network())'
+                 if not args.weights else f'synthetic: self-play from STARTING_FEN, trained checkpoint sha256 {weights_sha}'),
+        'config': {'workload': (f'{G} parallel self-play games per GPU, {sims} sims/move, random-init policy net '
+                                f'(BASELINE config 2; config 4 = 8 GPUs x 4096)') if not args.weights else
+                               (f'{G} parallel self-play games per GPU, {sims} sims/move, trained checkpoint '
+                                f'(BASELINE config 3)'),
                    'games_per_gpu': G, 'sims_per_move': sims, 'parallelism': f'games sharded over {world} GPU(s)'},
         'sims_per_s': tot['sims'] / dt,
         'nn_evals_per_s': tot['nn_evals'] / dt,

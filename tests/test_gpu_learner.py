@@ -168,8 +168,9 @@ def test_loop_two_iterations_single_gpu():
 def test_graph_captured_update_equals_eager_update():
     """The HIP-graph learner step (capturable AdamW, warm-up undone) takes the same steps as the
     eager loop (lr 1e-3, where AdamW is smooth):
-      * exactly one AdamW step per batch, and every weight within 1e-4 of the eager run (warm-up
-        or capture steps left in place would move weights by >= 3 AdamW steps, ~3e-3);
+      * exactly one AdamW step per batch, and every weight (but the noise-driven conv biases
+        before BatchNorm) within 1e-4 of the eager run (warm-up or capture steps left in place
+        would move weights by >= 3 AdamW steps, ~3e-3);
       * the same loss trace: the first loss (before any step) to 1e-6, later ones to 1e-3 (GPU
         backward reductions are not bitwise deterministic run to run)."""
     import torch
@@ -202,7 +203,10 @@ def test_graph_captured_update_equals_eager_update():
     assert len(l0) == len(l1) == 5
     assert abs(l0[0] - l1[0]) <= 1e-6 * abs(l0[0])
     assert np.allclose(l0, l1, rtol=1e-3)
-    assert max(float((weights[0][k] - weights[1][k]).abs().max()) for k in weights[0]) <= 1e-4
+    # conv biases that feed a BatchNorm have a zero gradient up to rounding noise, which AdamW
+    # normalises into +-lr steps in either run alike: they are excluded
+    keys = [k for k in weights[0] if not k.endswith('layers.0.bias')]
+    assert max(float((weights[0][k] - weights[1][k]).abs().max()) for k in keys) <= 1e-4
 
 
 def test_loop_with_arena_gate():
