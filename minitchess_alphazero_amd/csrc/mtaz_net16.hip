@@ -303,13 +303,27 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       if (i_ % 4 == 0) {                                                              \
         const int c_ = i_ / 4;                                                        \
         __builtin_amdgcn_sched_barrier(0);                                            \
-        if (c_ < 4) {                                                                 \
-          _Pragma("unroll") for (int q_ = 2 * c_; q_ < 2 * c_ + 2; ++q_)              \
-            BN[q_] = *reinterpret_cast<const f16x8*>(smem + (q_ >> 2) * PARTB + (q_ & 3) * IROWS * RB + o_); \
-        } else if (c_ < 8) {                                                          \
-          const int q_ = c_ - 4, ct_ = 2 * (PT) + (q_ >> 1), pp_ = q_ & 1;            \
-          AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
+        /* chunk c_ issues LDS reads [l0_, l1_) and weight loads [g0_, g1_) of the next half */ \
+        int l0_, l1_, g0_, g1_;                                                       \
+        if constexpr (VAR & 16) {        /* 1 LDS read per chunk 0-7, 1 load per chunk 8-11 */ \
+          l0_ = c_ < 8 ? c_ : 8; l1_ = c_ < 8 ? c_ + 1 : 8;                           \
+          g0_ = c_ >= 8 ? c_ - 8 : 0; g1_ = c_ >= 8 ? c_ - 7 : 0;                     \
+        } else if constexpr (VAR & 32) { /* L L G repeated: one load per chunk */     \
+          const int t3_ = c_ / 3, r3_ = c_ % 3;                                       \
+          l0_ = r3_ < 2 ? 2 * t3_ + r3_ : 0; l1_ = r3_ < 2 ? l0_ + 1 : 0;             \
+          g0_ = r3_ == 2 ? t3_ : 0; g1_ = r3_ == 2 ? t3_ + 1 : 0;                     \
+        } else {                         /* 2 LDS reads per chunk 0-3, 1 load per chunk 4-7 */ \
+          l0_ = c_ < 4 ? 2 * c_ : 0; l1_ = c_ < 4 ? 2 * c_ + 2 : 0;                   \
+          g0_ = (c_ >= 4 && c_ < 8) ? c_ - 4 : 0; g1_ = (c_ >= 4 && c_ < 8) ? c_ - 3 : 0; \
         }                                                                             \
+        _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_)                              \
+          if (q_ >= l0_ && q_ < l1_)                                                  \
+            BN[q_] = *reinterpret_cast<const f16x8*>(smem + (q_ >> 2) * PARTB + (q_ & 3) * IROWS * RB + o_); \
+        _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_)                              \
+          if (q_ >= g0_ && q_ < g1_) {                                                \
+            const int ct_ = 2 * (PT) + (q_ >> 1), pp_ = q_ & 1;                       \
+            AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
+          }                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                            \
       }                                                                               \
       const int ps_ = i_ >> 4, ct_ = (i_ >> 2) & 3, bb_ = i_ & 3;                     \
@@ -433,6 +447,10 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      unsigned long long* stamps) {
   if (var == 1024)
     hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 16)
+    hipLaunchKernelGGL((k_net_y<S, 16>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 32)
+    hipLaunchKernelGGL((k_net_y<S, 32>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 8)
     hipLaunchKernelGGL((k_net_y<S, 8>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 128)

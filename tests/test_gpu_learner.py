@@ -165,20 +165,40 @@ def test_loop_two_iterations_single_gpu():
     assert not torch.equal(w0, w2)
 
 
+def test_graph_capture_leaves_state_untouched():
+    """Capturing the learner step runs warm-up steps; afterwards the weights, BatchNorm buffers
+    and AdamW state must be exactly what they were before (so replays are the reference's
+    steps)."""
+    import torch
+    from minitchess_alphazero_amd.learner import ResidentBatches, SimpleAlphaZeroLearner
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network().train().cuda()
+    lrn = SimpleAlphaZeroLearner(None, 36, net, 32, 1, {'lr': 0.2}, device='cuda')
+    opt = torch.optim.AdamW(net.parameters(), lr=0.2, capturable=True)
+    data = ResidentBatches(_rows(2)[:100], 'cuda')
+    before = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    step = lrn._graph_step(net, opt, data)
+    for k, v in net.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    for st in opt.state.values():
+        for t in st.values():
+            assert not torch.is_tensor(t) or not t.any()
+    step(list(range(32)))                      # one replay = one step
+    assert {float(st['step']) for st in opt.state.values()} == {1.0}
+
+
 def test_graph_captured_update_equals_eager_update():
-    """The HIP-graph learner step (capturable AdamW, warm-up undone) takes the same steps as the
-    eager loop (lr 1e-3, where AdamW is smooth):
-      * exactly one AdamW step per batch, and every weight (but the noise-driven conv biases
-        before BatchNorm) within 1e-4 of the eager run (warm-up or capture steps left in place
-        would move weights by >= 3 AdamW steps, ~3e-3);
-      * the same loss trace: the first loss (before any step) to 1e-6, later ones to 1e-3 (GPU
-        backward reductions are not bitwise deterministic run to run)."""
+    """The HIP-graph learner update takes the same steps as the eager loop: exactly one AdamW
+    step per batch, the first loss (before any step) bitwise equal, later losses within 1e-3
+    relative (GPU training is not bitwise reproducible run to run: backward convolutions
+    accumulate in varying order)."""
     import torch
     from minitchess_alphazero_amd.learner import SimpleAlphaZeroLearner
     from minitchess_alphazero_amd.network import Network
     rows = _rows(3)[:150]
-    traces, weights = [], []
-    for graphs in (False, True):
+
+    def run(graphs):
         torch.manual_seed(0)
         net = Network()
         lrn = SimpleAlphaZeroLearner(None, 36, net, 32, 1, {'lr': 1e-3}, device='cuda')
@@ -197,16 +217,11 @@ def test_graph_captured_update_equals_eager_update():
             torch.optim.AdamW.__init__ = orig
         steps = {float(st['step']) for st in seen['opt'].state.values()}
         assert steps == {5.0}, steps                   # 4 graph replays + 1 eager tail batch
-        traces.append(np.array(lrn.last_losses))
-        weights.append({k: v.detach().float().cpu() for k, v in net.named_parameters()})
-    l0, l1 = traces
-    assert len(l0) == len(l1) == 5
-    assert abs(l0[0] - l1[0]) <= 1e-6 * abs(l0[0])
-    assert np.allclose(l0, l1, rtol=1e-3)
-    # conv biases that feed a BatchNorm have a zero gradient up to rounding noise, which AdamW
-    # normalises into +-lr steps in either run alike: they are excluded
-    keys = [k for k in weights[0] if not k.endswith('layers.0.bias')]
-    assert max(float((weights[0][k] - weights[1][k]).abs().max()) for k in keys) <= 1e-4
+        return np.array(lrn.last_losses)
+
+    le, lg = run(False), run(True)
+    assert len(le) == len(lg) == 5 and le[0] == lg[0]
+    assert np.allclose(lg, le, rtol=1e-3)
 
 
 def test_loop_with_arena_gate():
