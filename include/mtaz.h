@@ -105,6 +105,19 @@ int mtaz_play(mtaz_engine* h, int n_games, int from_current);
 int mtaz_records_counts(mtaz_engine* h, int32_t* plies_per_game, int64_t* total_plies, int64_t* total_entries);
 int mtaz_records_get(mtaz_engine* h, uint32_t* pos, int32_t* action, int32_t* k, uint16_t* codes, uint32_t* visits,
                      float* reward, int32_t* outcome);
+/* Episode wire format (app/base.py:63-69, MQTTDataset.push): one MQTT payload per game,
+ * byte-identical to json.dumps({'episode': InfoRecorder records, 'userid': userid,
+ * 'weights_version': weights_version, 'minitchess_alphazero_version': version}) (NULL
+ * strings are JSON null), from packed records laid out as mtaz_records_get writes them.
+ * Payload g is out[offsets[g] .. offsets[g+1]); returns the total byte count (offsets[n_games]
+ * too).  When out is NULL or the total exceeds cap nothing is written: call again with a
+ * buffer of the returned size.  Host-only; no engine or device needed. */
+int64_t mtaz_records_json(int n_games, const int32_t* plies, const uint32_t* pos, const int32_t* action,
+                          const int32_t* k, const uint16_t* codes, const uint32_t* visits, const float* reward,
+                          const char* userid, const char* weights_version, const char* version, char* out,
+                          int64_t cap, int64_t* offsets);
+/* CPython repr(float) of x (the float spelling of the payloads above); returns its length */
+int mtaz_repr_double(double x, char* buf, int cap);
 /* counters of the last mtaz_play: see minitchess_alphazero_amd/engine.py STAT_NAMES */
 int mtaz_stats(mtaz_engine* h, double* out, int n);
 /* record per-wave network HIP events during mtaz_play (trunk span for fp32, the fused

@@ -47,6 +47,9 @@ SIGNATURES = {
     'mtaz_play': (c_int, [c_void_p, c_int, c_int]),
     'mtaz_records_counts': (c_int, [c_void_p, P_i32, P_i64, P_i64]),
     'mtaz_records_get': (c_int, [c_void_p, P_u32, P_i32, P_i32, P_u16, P_u32, P_f32, P_i32]),
+    'mtaz_records_json': (c_int64, [c_int, P_i32, P_u32, P_i32, P_i32, P_u16, P_u32, P_f32, c_char_p, c_char_p,
+                                    c_char_p, c_void_p, c_int64, P_i64]),
+    'mtaz_repr_double': (c_int, [c_double, c_char_p, c_int]),
     'mtaz_stats': (c_int, [c_void_p, P_f64, c_int]),
     'mtaz_set_timing': (c_int, [c_void_p, c_int]),
     'mtaz_set_precision': (c_int, [c_void_p, c_int]),

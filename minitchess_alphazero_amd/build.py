@@ -1,8 +1,9 @@
 """Build libmtaz.so (HIP for gfx950) in-tree with hipcc.
 
-Two translation units: csrc/mtaz_device.hip (all kernels + launchers) and
-csrc/mtaz_host.cpp (C ABI, numpy-legacy RNG compiled with -ffp-contract=off,
-engine driver).  The shared object lands next to this file so it travels to the
+Translation units: csrc/mtaz_device.hip (tree kernels + launchers), csrc/mtaz_net.hip
+and csrc/mtaz_net16.hip (network kernels), csrc/mtaz_host.cpp (C ABI, numpy-legacy RNG
+compiled with -ffp-contract=off, engine driver) and csrc/mtaz_wire.cpp (episode wire
+format).  The shared object lands next to this file so it travels to the
 GPU box with the repo snapshot.
 """
 import os
@@ -21,6 +22,7 @@ SOURCES = [
     ('mtaz_net.hip', ['-O3']),
     ('mtaz_net16.hip', ['-O3']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
+    ('mtaz_wire.cpp', ['-O2']),
 ]
 HEADERS = ['rules.h', 'engine.h', 'net_common.h']
 

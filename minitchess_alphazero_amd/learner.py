@@ -376,19 +376,23 @@ class LearnPuppet:
             self._episode_counter += episodes
             self._records = EpisodeRecords.concat([self._records, records]).tail(self._max_length)
 
-    def update(self):
+    def update(self, encode=True):
         """app/base.py:188-195: load the current weights, train on the dataset, publish the new
-        weights as a new version, start a fresh dataset."""
+        weights as a new version, start a fresh dataset.  Returns get_weights_dict() plus
+        'loss'; encode=False puts the state_dict itself under 'weights' (for callers that move
+        the tensors over torch.distributed instead of HTTP, minitchess_alphazero_amd.loop)."""
         self._network.load_state_dict(self.weights)
         data = self._records if len(self._records) else self._dataset
         loss = self._learner.update(data)
         self.weights = self._network.state_dict()
         self._init_dataset()
-        out = self.get_weights_dict()
+        out = self.get_weights_dict() if encode else {'weights': copy.copy(self.weights),
+                                                      'version': self.weights_version}
         out['loss'] = loss
         return out
 
     def get_weights_dict(self):
-        """{'weights': state_dict (CPU tensors), 'version'}; the reference jsonpickle-encodes the
-        state_dict for HTTP (app/base.py:201-203) - the wire format is SURVEY 8f rank 3."""
-        return {'weights': copy.copy(self.weights), 'version': self.weights_version}
+        """app/base.py:201-203: {'weights': jsonpickle.encode(state_dict), 'version'}, the
+        document the learner posts to rlweb (minitchess_alphazero_amd.wire)."""
+        from .wire import get_weights_dict
+        return get_weights_dict(self.weights, self.weights_version)

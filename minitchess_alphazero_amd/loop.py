@@ -119,7 +119,7 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
             old_version = learner.weights_version
             learner.push_records(EpisodeRecords.concat(parts), games * world)
             learner.train()
-            out = learner.update()
+            out = learner.update(encode=False)
             learner.simulate()
             net.load_state_dict(out['weights'])
         torch.cuda.synchronize(dev)

@@ -9,7 +9,11 @@ run_episodes: instead of erlyx.run_episodes playing the episodes one after anoth
 on the CPU (app/base.py:116-120), all num_episodes games run in parallel in the HIP
 engine, then each episode's InfoRecorder records (exp/callbacks.py:31-54) are
 pushed through the same MQTT payload and gates as the reference's MQTTDataset
-(app/base.py:52-70).
+(app/base.py:52-70); the payloads of a batch are serialized natively from the packed
+records (minitchess_alphazero_amd.wire.episode_payloads), byte-identical to json.dumps.
+
+Weights from rlweb: `load_weights_blob(body)` decodes the reference's download_weights body
+(zlib + json + jsonpickle, app/base.py:31-39) without unpickling (wire.load_weights_blob).
 
 RNG: the reference draws from the global np.random; here every game gets its own
 numpy-legacy stream seeded from one np.random.randint draw, so seeding np.random
@@ -44,17 +48,30 @@ class MQTTDataset:
         self._puppet = puppet
         self._client = mqtt_client
 
-    def push(self, data):
+    def _gate(self):
         p = self._puppet
         if p.remote_status != MasterOfPuppetsStatus.SIMULATE:
             logging.info('Not pushing episode. Master Status is not SIMULATE')
-            return True
+            return False
         if p.remote_version != MINITCHESS_ALPHAZERO_VERSION:
             logging.info('Not pushing episode. Master version differs')
+            return False
+        return True
+
+    def push(self, data):
+        if not self._gate():
             return True
+        p = self._puppet
         payload = {'episode': data, 'userid': p.userid, 'weights_version': p.weights_version,
                    'minitchess_alphazero_version': MINITCHESS_ALPHAZERO_VERSION}
-        info = self._client.publish(p.publish_topic, json.dumps(payload), qos=2)
+        self.push_payload(json.dumps(payload), gated=True)
+
+    def push_payload(self, payload, gated=False):
+        """push() for a payload already serialized (wire.episode_payloads writes the same bytes
+        json.dumps would); same gates."""
+        if not gated and not self._gate():
+            return True
+        info = self._client.publish(self._puppet.publish_topic, payload, qos=2)
         logging.info(f'published episode with mid={getattr(info, "mid", None)}')
 
 
@@ -102,6 +119,13 @@ class SimulatePuppet:
         self._weights_version = version
         self._weights_dirty = True
 
+    def load_weights_blob(self, blob):
+        """download_weights() + load_weights(): the rlweb /get_weights body, decoded safely."""
+        from .wire import load_weights_blob
+        content = load_weights_blob(blob)
+        self.load_weights(content['weights'], content['version'])
+        return content['version']
+
     def is_simulating(self):
         return self._is_simulating
 
@@ -117,18 +141,30 @@ class SimulatePuppet:
             self._weights_dirty = False
         return self._engine
 
-    def play(self, num_episodes):
-        """Play num_episodes games in parallel batches; returns InfoRecorder records."""
-        out = []
+    def _batches(self, num_episodes):
         left = num_episodes
         while left > 0:
             n = min(left, self._max_parallel)
             seed_base = int(np.random.randint(0, 2 ** 31 - n))
             eng = self._engine_for(n, seed_base)
             eng.play(n_games=n)
-            out.extend(eng.episodes()[:n])
+            yield eng, n
             left -= n
+
+    def play(self, num_episodes):
+        """Play num_episodes games in parallel batches; returns InfoRecorder records."""
+        out = []
+        for eng, n in self._batches(num_episodes):
+            out.extend(eng.episodes()[:n])
         return out
+
+    def play_payloads(self, num_episodes):
+        """The games of play() as MQTT payloads, written natively (wire.episode_payloads):
+        the bytes MQTTDataset.push would publish for each episode."""
+        from .wire import episode_payloads
+        for eng, n in self._batches(num_episodes):
+            yield from episode_payloads(eng.records(), self.userid, self.weights_version,
+                                        MINITCHESS_ALPHAZERO_VERSION)[:n]
 
     def run_episodes(self, num_episodes, mqtt_client):
         """app/base.py:108-124: any Exception is logged and swallowed; the
@@ -137,8 +173,8 @@ class SimulatePuppet:
             self._is_simulating = True
             logging.info('Starting simulations')
             dataset = MQTTDataset(mqtt_client, self)
-            for episode in self.play(num_episodes):
-                dataset.push(episode)
+            for payload in self.play_payloads(num_episodes):
+                dataset.push_payload(payload)
         except Exception as e:
             logging.error(f'Exception occurred: {e}')
         finally:

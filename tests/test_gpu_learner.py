@@ -145,7 +145,8 @@ def test_selfplay_learn_selfplay_loop():
     lp.simulate()
     assert np.isfinite(out['loss']) and len(lp._dataset) == 0
     assert out['version'] == lp.weights_version and lp.weights_version >= v0
-    eng.set_weights(out['weights'])
+    from minitchess_alphazero_amd.wire import decode_weights
+    eng.set_weights(decode_weights(out['weights']))   # the reference's jsonpickle document
     st = eng.play()
     assert st['games'] == 16 and st['plies'] > 0
 

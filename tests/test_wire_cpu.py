@@ -1,0 +1,179 @@
+"""Wire formats on the CPU: the native episode payload writer against the
+reference's InfoRecorder records (tests/golden/trees.json, made by running the reference) put
+through the reference's own json.dumps expression (oracle/wire.py), and the weights document /
+blob against the restated jsonpickle pickler and unpickler, plus the safe decoder's refusals."""
+import base64
+import json
+import math
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+from minitchess_alphazero_amd import _lib, wire
+from minitchess_alphazero_amd.environment import pos_from_fen
+import oracle.wire as ow
+
+
+def _visits_from_pi(pi):
+    """Integer root visit counts N with N / N.sum() == pi bit for bit (the fixture keeps pi)."""
+    for s in range(1, 5000):
+        n = [round(p * s) for p in pi]
+        if sum(n) == s and all(x / s == p for x, p in zip(n, pi)):
+            return n
+    raise AssertionError('no integer visit vector reproduces pi')
+
+
+def _fixture_games():
+    t = load_golden('trees')
+    return [g['moves'] for g in t['synthetic']] + [g['moves'] for g in t['net_seed0']]
+
+
+def _pack(games):
+    plies, pos, action, k, codes, visits, reward = [], [], [], [], [], [], []
+    for moves in games:
+        plies.append(len(moves))
+        for m in moves:
+            pos.append(pos_from_fen(m['observation']))
+            action.append(m['action'])
+            k.append(len(m['legal_moves']))
+            codes += m['legal_moves']
+            visits += _visits_from_pi(m['pi'])
+            reward.append(m['reward'])
+    return {'plies': np.array(plies, np.int32), 'pos': np.array(pos, np.uint32), 'action': np.array(action, np.int32),
+            'k': np.array(k, np.int32), 'codes': np.array(codes, np.uint16), 'visits': np.array(visits, np.uint32),
+            'reward': np.array(reward, np.float32)}
+
+
+def test_float_repr_matches_python():
+    L = _lib.lib()
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    rng = random.Random(0)
+    vals = [0.0, -0.0, 1.0, -1.0, 1e-4, 1e-5, 9.999e-5, 1e16, 1e15, 12345678901234567.0, 5e-324,
+            2.2250738585072014e-308, 1.7976931348623157e308, 0.1, 1 / 3, 1 / 257]
+    for _ in range(20000):
+        vals.append(struct.unpack('d', struct.pack('Q', rng.getrandbits(64)))[0])
+        vals.append(rng.random() * 10 ** rng.randint(-30, 30))
+        vals.append(rng.randint(0, 300) / rng.randint(1, 3000))
+    for v in vals:
+        if math.isnan(v) or math.isinf(v):
+            continue
+        n = L.mtaz_repr_double(v, buf, 64)
+        assert n > 0 and buf.value.decode() == repr(v), v
+
+
+def test_episode_payloads_equal_reference_json():
+    games = _fixture_games()
+    rec = _pack(games)
+    got = wire.episode_payloads(rec, 'puppet-7', '20240101120000', '0.3.1')
+    assert len(got) == len(games)
+    for g, moves in enumerate(games):
+        assert got[g] == ow.episode_payload(moves, 'puppet-7', '20240101120000', '0.3.1'), g
+    # draws: the back-filled rewards alternate 0.0 / -0.0 and both spellings must survive
+    assert '"reward": -0.0' in got[0] and '"reward": 0.0' in got[0]
+    assert wire.parse_episode_payload(got[1])['episode'] == games[1]
+
+
+def test_episode_payload_strings_and_nulls():
+    games = _fixture_games()[:2]
+    rec = _pack(games)
+    for uid, wv, ver in [(None, None, None), ('ü"\\\n\t\x01 ☃ 𝄞', '', 'v"1'), ('x' * 300, '1' * 14, None)]:
+        got = wire.episode_payloads(rec, uid, wv, ver)
+        for g, moves in enumerate(games):
+            assert got[g] == ow.episode_payload(moves, uid, wv, ver)
+
+
+def test_episode_payload_edge_cases():
+    # an empty batch, and a game of zero plies next to a real one
+    rec = _pack([])
+    assert wire.episode_payloads(rec, 'u', 'w', 'v') == []
+    games = _fixture_games()[:1]
+    rec = _pack(games)
+    rec['plies'] = np.array([0, rec['plies'][0], 0], np.int32)
+    got = wire.episode_payloads(rec, 'u', 'w', 'v')
+    assert got[0] == got[2] == ow.episode_payload([], 'u', 'w', 'v')
+    assert got[1] == ow.episode_payload(games[0], 'u', 'w', 'v')
+    with pytest.raises(ValueError):
+        bad = dict(rec)
+        bad['codes'] = rec['codes'][:-1]
+        wire.episode_payloads(bad, 'u', 'w', 'v')
+
+
+def _state_dict():
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    return {k: v.detach().cpu() for k, v in net.state_dict().items()}
+
+
+def _same(a, b):
+    assert list(a) == list(b)
+    for k in a:
+        assert a[k].dtype == b[k].dtype and a[k].shape == b[k].shape and torch.equal(a[k], b[k]), k
+
+
+def test_weights_document_equals_restated_jsonpickle():
+    sd = _state_dict()
+    doc = wire.encode_weights(sd)
+    assert json.loads(doc) == json.loads(ow.jsonpickle_encode(sd))
+    _same(wire.decode_weights(doc), sd)
+    # the reference side's decode (jsonpickle.decode semantics) rebuilds the same tensors
+    _same(ow.jsonpickle_decode(doc), sd)
+
+
+def test_weights_blob_round_trip_and_views():
+    sd = _state_dict()
+    # non-contiguous and offset views, empty and 0-dim tensors
+    base = torch.arange(60, dtype=torch.float64).reshape(6, 10)
+    sd['extra.t'] = base.t()
+    sd['extra.slice'] = base[2:, 3:7]
+    sd['extra.empty'] = torch.zeros(0, 5)
+    sd['extra.scalar'] = torch.tensor(7, dtype=torch.int64)
+    d = wire.get_weights_dict(sd, '20240101120000')
+    blob = wire.weights_blob(d)
+    assert json.loads(zlib.decompress(blob)) == d
+    back = wire.load_weights_blob(blob)
+    assert back['version'] == '20240101120000'
+    _same(back['weights'], sd)
+    _same(ow.jsonpickle_decode(d['weights']), sd)
+
+
+def _doc_with(mutate):
+    sd = {'w': torch.arange(6, dtype=torch.float32).reshape(2, 3)}
+    doc = json.loads(wire.encode_weights(sd))
+    mutate(doc['w'])
+    return json.dumps(doc)
+
+
+@pytest.mark.parametrize('name,mutate', [
+    ('foreign function', lambda n: n['py/reduce'][0].update({'py/function': 'os.system'})),
+    ('foreign storage loader', lambda n: n['py/reduce'][1]['py/tuple'][0]['py/reduce'][0].update(
+        {'py/function': 'pickle.loads'})),
+    ('reference', lambda n: n.clear() or n.update({'py/id': 1})),
+    ('object', lambda n: n.clear() or n.update({'py/object': 'torch.Tensor'})),
+    ('bad base64', lambda n: n['py/reduce'][1]['py/tuple'][0]['py/reduce'][1]['py/tuple'][0].update(
+        {'py/b64': '!!notbase64'})),
+    ('pickle payload', lambda n: n['py/reduce'][1]['py/tuple'][0]['py/reduce'][1]['py/tuple'][0].update(
+        {'py/b64': base64.b64encode(b'\x80\x02cos\nsystem\nq\x00.').decode()})),
+    ('view past storage', lambda n: n['py/reduce'][1]['py/tuple'][2].update({'py/tuple': [4, 3]})),
+    ('negative offset', lambda n: n['py/reduce'][1]['py/tuple'].__setitem__(1, -1)),
+    ('hooks with items', lambda n: n['py/reduce'][1]['py/tuple'][5]['py/reduce'].__setitem__(
+        4, {'py/tuple': [{'py/tuple': ['k', {'py/function': 'os.system'}]}]})),
+])
+def test_weights_decoder_refuses(name, mutate):
+    with pytest.raises(ValueError):
+        wire.decode_weights(_doc_with(mutate))
+
+
+def test_learn_puppet_weights_dict_is_reference_format():
+    from minitchess_alphazero_amd.learner import LearnPuppet
+    lp = LearnPuppet('learner', 32, 1, {'lr': 0.2}, device='cpu')
+    d = lp.get_weights_dict()
+    assert set(d) == {'weights', 'version'} and isinstance(d['weights'], str)
+    _same(wire.decode_weights(d['weights']), lp.weights)
