@@ -191,7 +191,7 @@ def test_graph_capture_leaves_state_untouched():
 
 def test_graph_captured_update_equals_eager_update():
     """The HIP-graph learner update takes the same steps as the eager loop: exactly one AdamW
-    step per batch, the first loss (before any step) bitwise equal, later losses within 1e-3
+    step per batch, the first loss (before any step) within 1e-6, later losses within 1e-3
     relative (GPU training is not bitwise reproducible run to run: backward convolutions
     accumulate in varying order)."""
     import torch
@@ -221,7 +221,9 @@ def test_graph_captured_update_equals_eager_update():
         return np.array(lrn.last_losses)
 
     le, lg = run(False), run(True)
-    assert len(le) == len(lg) == 5 and le[0] == lg[0]
+    # the first loss is the same forward on the same weights; MIOpen may still pick a different
+    # algorithm in the two runs (seen: 7.7e-8 relative), so 1e-6, not bitwise
+    assert len(le) == len(lg) == 5 and abs(le[0] - lg[0]) <= 1e-6 * abs(le[0])
     assert np.allclose(lg, le, rtol=1e-3)
 
 
