@@ -76,6 +76,15 @@ int mtaz_legal_batch(int device, const uint32_t* d_pos, int n, uint32_t rules_fl
                      int32_t* d_counts, uint32_t* d_masks, int32_t* d_outcomes, void* stream);
 /* Network.process_observation for a batch (exp/policy.py:96-105) */
 int mtaz_encode_batch(int device, const uint32_t* d_pos, int n, uint8_t* d_tokens, float* d_clocks, void* stream);
+/* Replay memory ingest (exp/dataset.py:6-20 push + the row half of collate_fn,
+ * exp/learner.py:23-37), all pointers device memory: row i of a packed record batch (pos,
+ * legal list length k, entry start e0 into codes / visits, reward) is written to ring slot
+ * (head + i) % cap as tokens [60] u8, clock f32, dense pi [554] f32 (N / N.sum() in float64,
+ * repeated codes: last entry wins) and reward f32.  n <= cap; d_e0[i] + d_k[i] must lie inside
+ * codes / visits (the caller's prefix sum).  Enqueued on `stream` (no sync). */
+int mtaz_replay_put(int device, int n, const uint32_t* d_pos, const int32_t* d_k, const int64_t* d_e0,
+                    const uint16_t* d_codes, const uint32_t* d_visits, const float* d_reward, int64_t cap,
+                    int64_t head, uint8_t* d_tokens, float* d_clocks, float* d_pi, float* d_reward_out, void* stream);
 
 /* ---- engine ------------------------------------------------------------------------- */
 typedef struct mtaz_engine mtaz_engine;

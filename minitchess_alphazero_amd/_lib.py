@@ -40,6 +40,8 @@ SIGNATURES = {
     'mtaz_rng_randint': (c_int64, [c_void_p, c_int64]),
     'mtaz_legal_batch': (c_int, [c_int, c_void_p, c_int, c_uint32, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mtaz_encode_batch': (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    'mtaz_replay_put': (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                  c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mtaz_create': (c_void_p, [c_int, c_int, c_int, c_double, c_int, c_double, c_double, c_uint64, c_int, c_uint32, c_int]),
     'mtaz_destroy': (None, [c_void_p]),
     'mtaz_set_weights': (c_int, [c_void_p, POINTER(c_void_p), P_i64, c_int]),

@@ -154,6 +154,9 @@ int dev_upload_codec(const Codec& c);
 void launch_legal_batch(const Pos* pos, int n, uint32_t flags, int move_cap, uint16_t* codes, int32_t* counts,
                         uint32_t* masks, int32_t* outcomes, hipStream_t s);
 void launch_encode_batch(const Pos* pos, int n, uint8_t* tokens, float* clocks, hipStream_t s);
+void launch_replay_put(const Pos* pos, const int32_t* k, const int64_t* e0, const uint16_t* codes,
+                       const uint32_t* visits, const float* reward, int n, int64_t cap, int64_t head,
+                       uint8_t* tokens, float* clocks, float* pi, float* reward_out, hipStream_t s);
 void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s);
 void launch_move_begin(const Dev& d, hipStream_t s);
 void launch_select(const Dev& d, int sim, hipStream_t s);

@@ -141,6 +141,54 @@ __global__ void k_encode_batch(const Pos* __restrict__ pos, int n, uint8_t* __re
   clocks[i] = encode_clock(b);
 }
 
+// Replay memory ingest (exp/dataset.py:6-20 + the row half of collate_fn,
+// exp/learner.py:23-37): row i of a packed record batch is encoded into ring slot
+// (head + i) % cap: tokens + clock as k_encode_batch, the dense 554-wide pi target
+// pi[code] = float32(N / N.sum()) in float64 (exp/policy.py:120), and the reward.  Legal lists
+// are sorted, so a repeated code (promotions) is a run of equal codes, and the reference's
+// last-write-wins assignment keeps the run's last entry: each code is written once.  One
+// wavefront per row; the row is built in LDS and stored coalesced.
+__global__ void k_replay_put(const Pos* __restrict__ pos, const int32_t* __restrict__ k, const int64_t* __restrict__ e0,
+                             const uint16_t* __restrict__ codes, const uint32_t* __restrict__ visits,
+                             const float* __restrict__ reward, int n, int64_t cap, int64_t head,
+                             uint8_t* __restrict__ tokens, float* __restrict__ clocks, float* __restrict__ pi,
+                             float* __restrict__ reward_out) {
+  __shared__ float row[NUM_ACTIONS];
+  const int i = blockIdx.x, lane = threadIdx.x;
+  if (i >= n) return;
+  const int64_t slot = (head + i) % cap;
+  const int kk = k[i];
+  const int64_t e = e0[i];
+  for (int c = lane; c < NUM_ACTIONS; c += 64) row[c] = 0.f;
+  uint64_t sum = 0;
+  for (int j = lane; j < kk; j += 64) sum += visits[e + j];
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  __syncthreads();
+  for (int j = lane; j < kk; j += 64) {
+    const uint16_t c = codes[e + j];
+    if (j == kk - 1 || codes[e + j + 1] != c) row[c] = (float)((double)visits[e + j] / (double)sum);
+  }
+  __syncthreads();
+  float* out = pi + slot * NUM_ACTIONS;
+  for (int c = lane; c < NUM_ACTIONS; c += 64) out[c] = row[c];
+  if (lane == 0) {
+    const BB b = unpack(pos[i]);
+    uint8_t t[60];
+    encode_tokens(b, t);
+    for (int j = 0; j < 60; ++j) tokens[slot * 60 + j] = t[j];
+    clocks[slot] = encode_clock(b);
+    reward_out[slot] = reward[i];
+  }
+}
+
+void launch_replay_put(const Pos* pos, const int32_t* k, const int64_t* e0, const uint16_t* codes,
+                       const uint32_t* visits, const float* reward, int n, int64_t cap, int64_t head,
+                       uint8_t* tokens, float* clocks, float* pi, float* reward_out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_replay_put, dim3(n), dim3(64), 0, s, pos, k, e0, codes, visits, reward, n, cap, head, tokens,
+                     clocks, pi, reward_out);
+}
+
 void launch_legal_batch(const Pos* pos, int n, uint32_t flags, int move_cap, uint16_t* codes, int32_t* counts,
                         uint32_t* masks, int32_t* outcomes, hipStream_t s) {
   if (n <= 0) return;

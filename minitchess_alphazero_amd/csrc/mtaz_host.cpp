@@ -407,6 +407,18 @@ extern "C" int mtaz_legal_batch(int device, const uint32_t* d_pos, int n, uint32
   return 0;
 }
 
+extern "C" int mtaz_replay_put(int device, int n, const uint32_t* d_pos, const int32_t* d_k, const int64_t* d_e0,
+                               const uint16_t* d_codes, const uint32_t* d_visits, const float* d_reward, int64_t cap,
+                               int64_t head, uint8_t* d_tokens, float* d_clocks, float* d_pi, float* d_reward_out,
+                               void* stream) {
+  if (n < 0 || cap <= 0 || head < 0 || n > cap) return set_err(MTAZ_E_FAIL, "replay_put: bad n/cap/head");
+  HIPCHK(hipSetDevice(device));
+  launch_replay_put(reinterpret_cast<const Pos*>(d_pos), d_k, d_e0, d_codes, d_visits, d_reward, n, cap, head, d_tokens,
+                    d_clocks, d_pi, d_reward_out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 extern "C" int mtaz_encode_batch(int device, const uint32_t* d_pos, int n, uint8_t* d_tokens, float* d_clocks, void* stream) {
   HIPCHK(hipSetDevice(device));
   launch_encode_batch(reinterpret_cast<const Pos*>(d_pos), n, d_tokens, d_clocks, (hipStream_t)stream);

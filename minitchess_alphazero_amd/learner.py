@@ -18,6 +18,7 @@ MQTT / HTTP transport (app/learner.py) is out of scope (wire formats 
 LearnPuppet keeps the state machine, the dataset and the versioned weights.
 """
 import copy
+import ctypes
 import logging
 from collections import deque
 from datetime import datetime
@@ -113,9 +114,101 @@ class ResidentBatches:
     def __len__(self):
         return self.pi.shape[0]
 
-    def batch(self, idx):
-        i = torch.as_tensor(idx, dtype=torch.long, device=self.device)
+    def gather(self, i):
+        """Rows at the device index tensor i (capturable in a HIP graph)."""
         return self.pi[i], self.tokens[i], self.clock[i], self.reward[i]
+
+    def batch(self, idx):
+        return self.gather(torch.as_tensor(idx, dtype=torch.long, device=self.device))
+
+
+class ReplayBuffer:
+    """SimpleAlphaZeroDataset (exp/dataset.py:6-20) resident in HBM.
+
+    A ring of encoded rows: tokens [cap, 60] u8, clock [cap] f32, dense pi [cap, 554] f32,
+    reward [cap] f32 (2,284 B per row, so the reference's max_length of 1e6 rows is 2.3 GB).
+    push_records() uploads the packed records (EpisodeRecords: 20 B of position + 6 B per legal
+    entry per row) and one HIP launch (mtaz_replay_put) encodes them into the slots after the
+    newest row; past max_length the oldest rows are overwritten, the deque(maxlen) semantics.
+    Row i (0 = oldest, as deque indexing) lives in slot (head + i) % cap.  Batches are index
+    gathers on the device, so an update never re-encodes or re-uploads its dataset.  The
+    ring grows geometrically up to max_length (no up-front 2.3 GB allocation)."""
+
+    ROW_BYTES = 60 + 4 + 4 * NUM_ACTIONS + 4
+
+    def __init__(self, max_length, device, initial=1 << 16):
+        self.max_length = int(max_length)
+        self.device = torch.device(device)
+        if self.device.type != 'cuda':
+            raise RuntimeError('ReplayBuffer lives in GPU memory (HIP ingest kernel); use '
+                               'SimpleAlphaZeroDataset / ResidentBatches on the host')
+        self.cap = 0
+        self.head = 0
+        self.size = 0
+        self._alloc(min(self.max_length, initial))
+
+    def _alloc(self, cap):
+        dev = self.device
+        new = (torch.zeros((cap, 60), dtype=torch.uint8, device=dev), torch.zeros(cap, dtype=torch.float32, device=dev),
+               torch.zeros((cap, NUM_ACTIONS), dtype=torch.float32, device=dev),
+               torch.zeros(cap, dtype=torch.float32, device=dev))
+        if self.size:
+            order = (torch.arange(self.size, device=dev) + self.head) % self.cap
+            for dst, src in zip(new, (self._tokens, self._clock, self._pi, self._reward)):
+                dst[:self.size] = src[order]
+        self._tokens, self._clock, self._pi, self._reward = new
+        self.cap, self.head = cap, 0
+
+    def __len__(self):
+        return self.size
+
+    def clear(self):
+        """A fresh, empty dataset (LearnPuppet._init_dataset) keeping the allocation."""
+        self.head = self.size = 0
+
+    def push_records(self, rec):
+        """Append packed rows (EpisodeRecords, host arrays) in order."""
+        dev = self.device
+        n = len(rec)
+        if n == 0:
+            return
+        k = torch.from_numpy(rec.k.astype(np.int32)).to(dev)
+        self.push_device(torch.from_numpy(rec.pos.view(np.int32)).to(dev), k,
+                         torch.from_numpy(rec.codes.view(np.int16)).to(dev),
+                         torch.from_numpy(rec.visits.view(np.int32)).to(dev),
+                         torch.from_numpy(rec.reward).to(dev))
+
+    def push_device(self, pos, k, codes, visits, reward):
+        """Append rows already on the device: pos [n,5] i32 (u32 bits), k [n] i32, codes [E]
+        i16 (u16 bits), visits [E] i32 (u32 bits), reward [n] f32."""
+        n = int(k.shape[0])
+        if n == 0:
+            return
+        e0 = torch.cumsum(k.to(torch.int64), 0) - k.to(torch.int64)
+        if n > self.max_length:                        # only the newest max_length rows survive
+            s = n - self.max_length
+            pos, k, e0, reward, n = pos[s:], k[s:], e0[s:], reward[s:], self.max_length
+        if self.size + n > self.cap and self.cap < self.max_length:
+            self._alloc(min(self.max_length, max(2 * self.cap, self.size + n)))
+        tail = (self.head + self.size) % self.cap
+        args = [c.contiguous() for c in (pos, k, e0, codes, visits, reward)]
+        _lib.check(_lib.lib().mtaz_replay_put(
+            self.device.index or 0, n, *[a.data_ptr() for a in args], self.cap, tail,
+            self._tokens.data_ptr(), self._clock.data_ptr(), self._pi.data_ptr(), self._reward.data_ptr(),
+            ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
+        over = max(0, self.size + n - self.cap)
+        self.size = min(self.cap, self.size + n)
+        self.head = (self.head + over) % self.cap
+
+    def gather(self, i):
+        """Rows i (device index tensor, 0 = oldest) -> (pi, tokens [.,2,6,5] i64, clock [.,1],
+        reward [.,1]); capturable in a HIP graph (head is fixed for an update)."""
+        j = (i + self.head) % self.cap if self.head else i
+        return (self._pi[j], self._tokens[j].long().reshape(-1, 2, 6, 5), self._clock[j].reshape(-1, 1),
+                self._reward[j].reshape(-1, 1))
+
+    def batch(self, idx):
+        return self.gather(torch.as_tensor(idx, dtype=torch.long, device=self.device))
 
 
 class EpisodeRecords:
@@ -238,12 +331,13 @@ class SimpleAlphaZeroLearner:
         BatchNorm buffers and optimizer state are then restored to their pre-warm-up values,
         so the replayed steps are the reference's steps; AdamW runs with capturable=True (its
         step count on the device).  A partial last batch runs eagerly."""
-        if isinstance(dataset, EpisodeRecords):
-            rows = dataset
-        else:
-            rows = dataset.get_memory() if hasattr(dataset, 'get_memory') else list(dataset)
         model = self._network.train().to(self._device)
-        data = ResidentBatches(rows, self._device)
+        if isinstance(dataset, ReplayBuffer):
+            data = dataset
+        else:
+            rows = dataset if isinstance(dataset, EpisodeRecords) else \
+                dataset.get_memory() if hasattr(dataset, 'get_memory') else list(dataset)
+            data = ResidentBatches(rows, self._device)
         use_graph = self.graphs and self._device.type == 'cuda' and len(data) >= self._batch_size
         optimizer = torch.optim.AdamW(model.parameters(), **self._optim_params,
                                       **({'capturable': True} if use_graph else {}))
@@ -281,8 +375,7 @@ class SimpleAlphaZeroLearner:
         saved = {k: v.detach().clone() for k, v in model.state_dict().items()}
 
         def body():
-            pib, tok, clk, rew = data.pi[static_idx], data.tokens[static_idx], data.clock[static_idx], \
-                data.reward[static_idx]
+            pib, tok, clk, rew = data.gather(static_idx)
             loss = alphazero_loss(model, pib, tok, clk, rew)
             optimizer.zero_grad(set_to_none=False)
             loss.backward()
@@ -323,6 +416,7 @@ class LearnPuppet:
     def __init__(self, userid, batch_size, epochs, optim_params, device=None, max_length=1_000_000):
         self._userid = userid
         self._max_length = max_length
+        self._replay = None
         self._dataset = None
         self._init_dataset()
         self._network = Network()
@@ -336,6 +430,8 @@ class LearnPuppet:
     def _init_dataset(self):
         self._dataset = SimpleAlphaZeroDataset(max_length=self._max_length)
         self._records = EpisodeRecords.concat([])
+        if getattr(self, '_replay', None) is not None:
+            self._replay.clear()
 
     @property
     def episode_counter(self):
@@ -371,10 +467,16 @@ class LearnPuppet:
             self._dataset.push(data)
 
     def push_records(self, records, episodes):
-        """push_data for packed rows (EpisodeRecords) of `episodes` episodes."""
+        """push_data for packed rows (EpisodeRecords) of `episodes` episodes.  On a GPU learner
+        the rows go straight into the HBM replay ring (ReplayBuffer), encoded on arrival."""
         if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
             self._episode_counter += episodes
-            self._records = EpisodeRecords.concat([self._records, records]).tail(self._max_length)
+            if self._learner._device.type == 'cuda':
+                if self._replay is None:
+                    self._replay = ReplayBuffer(self._max_length, self._learner._device)
+                self._replay.push_records(records)
+            else:
+                self._records = EpisodeRecords.concat([self._records, records]).tail(self._max_length)
 
     def update(self, encode=True):
         """app/base.py:188-195: load the current weights, train on the dataset, publish the new
@@ -382,7 +484,10 @@ class LearnPuppet:
         'loss'; encode=False puts the state_dict itself under 'weights' (for callers that move
         the tensors over torch.distributed instead of HTTP, minitchess_alphazero_amd.loop)."""
         self._network.load_state_dict(self.weights)
-        data = self._records if len(self._records) else self._dataset
+        if self._replay is not None and len(self._replay):
+            data = self._replay
+        else:
+            data = self._records if len(self._records) else self._dataset
         loss = self._learner.update(data)
         self.weights = self._network.state_dict()
         self._init_dataset()

@@ -128,3 +128,11 @@ def test_learn_puppet_state_machine():
     lp.simulate()
     assert lp.status == 'SIMULATE'
     assert lp.weights_version == v0 and set(lp.get_weights_dict()) == {'weights', 'version'}
+
+
+def test_replay_ring_refuses_host_device():
+    """The HBM replay ring has no host fallback: on a CPU device it must refuse loudly."""
+    import pytest
+    from minitchess_alphazero_amd.learner import ReplayBuffer
+    with pytest.raises(RuntimeError):
+        ReplayBuffer(100, 'cpu')
