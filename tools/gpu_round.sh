@@ -13,7 +13,7 @@ step() {   # step NAME TIMEOUT CMD...
   echo "[$name] rc=$rc"; tail -${TAIL:-4} $OUT/$name.log | cut -c1-600
   return $rc
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step bench 600 python bench.py || exit $?
 step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --no-cpu-baseline || exit $?
