@@ -184,7 +184,11 @@ def main():
         'roofline': {'bound': 'mfma', 'kernel': kernel, 'achieved': achieved,
                      'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
                      'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch,
-                     'mfma_passes': 3 if f16x3 else 1},
+                     'mfma_passes': 3 if f16x3 else 1,
+                     # the f16 MFMA FLOP the split actually issues (3 passes per algorithmic FLOP),
+                     # over the same dense f16 peak: the MFMA pipe's utilisation
+                     'issued_achieved': achieved * (3 if f16x3 else 1),
+                     'issued_frac': achieved * (3 if f16x3 else 1) / peak},
         # secondary roofline: the tree kernel k_select, HBM/latency-bound; algorithmic
         # bytes per simulation = SURVEY's estimate (path nodes: header + k edge reads + edge update,
         # leaf insert, hash probe, NN input) at k ~ 7.5, depth ~ 2

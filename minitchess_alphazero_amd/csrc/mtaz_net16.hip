@@ -49,7 +49,7 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
 // SA[2*ct + part], SB[part*8 + t] with t = 2*board + square tile.
 #define YMMA(SA, SB, WP, XP)                                                                          \
   {                                                                                                   \
-    _Pragma("unroll") for (int ct_ = 0; ct_ < 4; ++ct_)                                               \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < CT; ++ct_)                                              \
     _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_)                                                  \
       acc[ct_ * 8 + t_] = __builtin_amdgcn_mfma_f32_16x16x32_f16(SA[2 * ct_ + (WP)], SB[(XP) * 8 + t_], \
                                                                  acc[ct_ * 8 + t_], 0, 0, 0);         \
@@ -58,11 +58,16 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
 #define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
 
 // VAR (in-process A/B, tools/bench_net.py): 0 = product; 4, 8, 128: K-loop schedules (see the
-// trunk); 1024: the epilogue in unfused form (bit-identity reference for the product).
+// trunk); 1024: the epilogue in unfused form (bit-identity reference for the product);
+// 2048: 8 waves (2 per SIMD), each owning 32 output channels (CT = 2 channel tiles) instead of
+// 64, same boards, LDS image and weight stream (each weight fragment still loaded by one wave);
+// 4096 (with 2048): s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD item 4).
+template <int VAR>
+constexpr int kWaves = (VAR & 2048) ? 8 : 4;
 // In-process A/B on one MI355X, 4096 boards, before dynamic range: pinned half-steps (now 0)
 // 5.04 ms, whole steps (now 8) 5.01, 128 5.06, 4 5.25-5.34.
 template <bool STAMP, int VAR>
-__global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
+__global__ __launch_bounds__(64 * kWaves<VAR>, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
                                                   float* __restrict__ logits_out, float* __restrict__ values_out,
                                                   unsigned long long* __restrict__ stamps) {
@@ -70,8 +75,12 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
   if (b0 >= nb) return;
+  constexpr int NW = kWaves<VAR>, NT = 64 * NW, CT = 16 / NW;   // waves, threads, channel tiles per wave
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, n = lane & 15, g = lane >> 4;
+  if constexpr ((VAR & 4096) != 0) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   unsigned long long t_prev = 0, st_stem = 0, st_k = 0, st_epi = 0, st_heads = 0;
   unsigned long long t_start = 0, r_start = 0;
   if constexpr (STAMP) {
@@ -89,9 +98,9 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // the lane's output squares: n (tile 0) and p1 = 16 + n (tile 1; 30, 31 are padding)
   const int p1 = 16 + n;
   const int ph0 = n / 5, pw0 = n % 5, ph1 = p1 / 5, pw1 = p1 % 5;
-  f32x4v acc[32];
+  f32x4v acc[CT * 8];
 #pragma unroll
-  for (int i = 0; i < 32; ++i) acc[i] = (f32x4v){0};
+  for (int i = 0; i < CT * 8; ++i) acc[i] = (f32x4v){0};
   int overflow = 0;
 
   // Dynamic range.  The image holds x * 2^-xs in f16 hi/lo with one exponent xs per workgroup
@@ -127,8 +136,8 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     const float sseed = __builtin_ldexpf(s_next, xs - xo);
     float ymax = 0.f;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int co0 = 64 * wave + 16 * ct + 4 * g;
+    for (int ct = 0; ct < CT; ++ct) {
+      const int co0 = 16 * CT * wave + 16 * ct + 4 * g;
       const float4 bu = *reinterpret_cast<const float4*>(bias + co0);
       const float4 bv = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
 #pragma unroll
@@ -198,14 +207,14 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
 
   // ---------------- stem: conv3x3 8->256, K = 3 k-blocks of (4 taps x 8 channels) ----------
   char* simg = smem + IMGB;
-  stem_input(smem, simg, pos, b0, nb, W, tid);
+  stem_input<NT>(smem, simg, pos, b0, nb, W, tid);
   __syncthreads();
   {
-    const uint4* Ws = W.stemy + (size_t)(4 * wave) * 3 * 128 + lane;
+    const uint4* Ws = W.stemy + (size_t)(CT * wave) * 3 * 128 + lane;
     for (int kb = 0; kb < 3; ++kb) {
-      f16x8 SA[8], SB[16];
+      f16x8 SA[2 * CT], SB[16];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < CT; ++c) {
         SA[2 * c] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128]);
         SA[2 * c + 1] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128 + 64]);
       }
@@ -236,13 +245,13 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   constexpr bool HALVES = (VAR & (4 | 8)) == 0;
   constexpr int PD = 2, RS = 3, U = 6;
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
-  f16x8 A[RS][8], B[2][16], BH[2][8];
-  const uint4* Wl = W.convy + (size_t)(4 * wave) * KBY * 128 + lane;
+  f16x8 A[RS][2 * CT], B[2][16], BH[2][8];
+  const uint4* Wl = W.convy + (size_t)(CT * wave) * KBY * 128 + lane;
 #define LOAD_A(S, KB)                                                                 \
   {                                                                                   \
     const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
     const uint4* p_ = Wl + (size_t)kk_ * 128;                                         \
-    _Pragma("unroll") for (int c_ = 0; c_ < 4; ++c_) {                                \
+    _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_) {                               \
       S[2 * c_] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128]);                      \
       S[2 * c_ + 1] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128 + 64]);             \
     }                                                                                 \
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   }
 #define YMMA_H(SA, SB, PT, WP, XP)                                                                    \
   {                                                                                                   \
-    _Pragma("unroll") for (int ct_ = 0; ct_ < 4; ++ct_)                                               \
+    _Pragma("unroll") for (int ct_ = 0; ct_ < CT; ++ct_)                                              \
     _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                                              \
       acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(                         \
           SA[2 * ct_ + (WP)], SB[(XP) * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0);             \
@@ -299,7 +308,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     const int o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                \
     const int ka_ = ((KB) + PD) < KBY ? ((KB) + PD) : KBY - 1;                        \
     const uint4* pa_ = Wl + (size_t)ka_ * 128;                                        \
-    _Pragma("unroll") for (int i_ = 0; i_ < 48; ++i_) {                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < 12 * CT; ++i_) {                          \
       if (i_ % 4 == 0) {                                                              \
         const int c_ = i_ / 4;                                                        \
         __builtin_amdgcn_sched_barrier(0);                                            \
@@ -314,19 +323,19 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
           g0_ = r3_ == 2 ? t3_ : 0; g1_ = r3_ == 2 ? t3_ + 1 : 0;                     \
         } else {                         /* 2 LDS reads per chunk 0-3, 1 load per chunk 4-7 */ \
           l0_ = c_ < 4 ? 2 * c_ : 0; l1_ = c_ < 4 ? 2 * c_ + 2 : 0;                   \
-          g0_ = (c_ >= 4 && c_ < 8) ? c_ - 4 : 0; g1_ = (c_ >= 4 && c_ < 8) ? c_ - 3 : 0; \
+          g0_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 4 : 0; g1_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 3 : 0; \
         }                                                                             \
         _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_)                              \
           if (q_ >= l0_ && q_ < l1_)                                                  \
             BN[q_] = *reinterpret_cast<const f16x8*>(smem + (q_ >> 2) * PARTB + (q_ & 3) * IROWS * RB + o_); \
-        _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_)                              \
+        _Pragma("unroll") for (int q_ = 0; q_ < CT; ++q_)                             \
           if (q_ >= g0_ && q_ < g1_) {                                                \
-            const int ct_ = 2 * (PT) + (q_ >> 1), pp_ = q_ & 1;                       \
+            const int ct_ = (CT / 2) * (PT) + (q_ >> 1), pp_ = q_ & 1;                \
             AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
           }                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                            \
       }                                                                               \
-      const int ps_ = i_ >> 4, ct_ = (i_ >> 2) & 3, bb_ = i_ & 3;                     \
+      const int ps_ = i_ / (4 * CT), ct_ = (i_ >> 2) % CT, bb_ = i_ & 3;              \
       const int wp_ = ps_ == 2 ? 1 : 0, xp_ = ps_ == 1 ? 1 : 0;                       \
       acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(         \
           AC[2 * ct_ + wp_], BC[xp_ * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0); \
@@ -426,7 +435,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   if (overflow) atomicOr(D.pr.err, ERR_F16);
 
   // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
-  heads_reduce(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs));
+  heads_reduce<NT>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs));
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
@@ -447,6 +456,10 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      unsigned long long* stamps) {
   if (var == 1024)
     hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 2048)
+    hipLaunchKernelGGL((k_net_y<S, 2048>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 6144)
+    hipLaunchKernelGGL((k_net_y<S, 6144>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var == 16)
     hipLaunchKernelGGL((k_net_y<S, 16>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var == 32)

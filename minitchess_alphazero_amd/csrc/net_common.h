@@ -50,13 +50,14 @@ __device__ __forceinline__ float clock_of(const Pos& p) {
 // [part][board][row 31][8 ch f16], channel c = plane*4 + e of Embedding(7,4) applied to the
 // own / opponent token planes (exp/policy.py:71-74, encoder exp/environment.py:63-75).
 // Caller: __syncthreads() before reading.
+template <int NT = 256>
 __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* pos, int b0, int nb,
                                            const NetWeights& W, int tid) {
-  for (int i = tid; i < 2 * XB * 32; i += 256) {
+  for (int i = tid; i < 2 * XB * 32; i += NT) {
     const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
     *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
   }
-  for (int i = tid; i < 2 * XB * IROWS; i += 256) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 2 * XB * IROWS; i += NT) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
   if (tid < XB * 30) {
     const int bb = tid / 30, i = tid % 30;          // i = square index in the mover's view
@@ -84,16 +85,17 @@ __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* po
   }
 }
 
-// Heads, part 1 (all 256 threads): policy conv 256->2 and value conv 256->1 (1x1, BN folded,
-// ReLU) from the final image, the clock feature, the value MLP hidden layer and its
-// reduction.  Leaves fp [XB][64] (60 policy features + clock), red[bb*256] = value pre-tanh.
-// xscale: the image holds x / xscale (a power of two; k_net_y's dynamic range), 1 otherwise.
+// Heads, part 1 (all NT >= 256 threads of the workgroup): policy conv 256->2 and value conv
+// 256->1 (1x1, BN folded, ReLU) from the final image, the clock feature, the value MLP hidden
+// layer and its reduction.  Leaves fp [XB][64] (60 policy features + clock), red[bb*256] = value
+// pre-tanh.  xscale: the image holds x / xscale (a power of two; k_net_y's dynamic range).
+template <int NT = 256>
 __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0, int nb, const NetWeights& W,
                                              int tid, float xscale = 1.f) {
   float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
   float* fv = fp + XB * 64;                            // [XB][32]: vconv features (30) + clock
   float* red = fv + XB * 32;                           // [XB][256]
-  for (int t = tid; t < XB * 90; t += 256) {
+  for (int t = tid; t < XB * 90; t += NT) {
     const int bb = t / 90, o = (t % 90) / 30, p = t % 30;
     const float* wr = o < 2 ? W.pconv_w + o * 256 : W.vconv_w;
     float s = 0.f;
@@ -113,7 +115,7 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
     fv[tid * 32 + 30] = clk;
   }
   __syncthreads();
-  {
+  if (tid < 256) {
     const int j = tid;
 #pragma unroll
     for (int bb = 0; bb < XB; ++bb) {
@@ -138,6 +140,7 @@ __device__ __forceinline__ void heads_out(const Dev& D, char* smem, int b0, int 
                                           float* logits_out, float* values_out, int wave, int lane) {
   const float* fp = reinterpret_cast<const float*>(smem + IMGB);
   const float* red = fp + XB * 64 + XB * 32;
+  if (wave >= XB) return;
   const int bb = wave;
   const int b = b0 + bb;
   if (b >= nb) return;

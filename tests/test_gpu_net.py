@@ -26,7 +26,8 @@ def _softmax(x):
 # f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 8, 128);
 # f16x3-x* = k_net_x (32x32x16 MFMA, variant bit 512) and its schedules; fp32 = fp32 MFMA path
 NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4), 'f16x3-y128': ('f16x3', 128),
-               'f16x3-y8': ('f16x3', 8), 'f16x3-x': ('f16x3', 512)}
+               'f16x3-y8': ('f16x3', 8), 'f16x3-x': ('f16x3', 512), 'f16x3-y2048': ('f16x3', 2048),
+               'f16x3-y6144': ('f16x3', 6144)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
@@ -104,6 +105,27 @@ def test_mix_epilogue_bit_identical():
     eng.set_net_variant(0)
     l0, v0 = eng.evaluate(pos)
     eng.set_net_variant(1024)
+    l1, v1 = eng.evaluate(pos)
+    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
+@pytest.mark.parametrize('var', [2048, 6144])
+def test_eight_wave_build_bit_identical(var):
+    """The 8-wave build (2 waves per SIMD, 32 output channels per wave) issues every
+    accumulator's MFMAs in the product's order, so its logits and values are bitwise equal."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from minitchess_alphazero_amd.network import Network
+    from tests_positions import random_fens
+    import torch
+    eng = Engine(n_games=64, sims=8)
+    torch.manual_seed(0)
+    eng.set_weights(Network())
+    pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=6)])
+    eng.set_net_variant(0)
+    l0, v0 = eng.evaluate(pos)
+    eng.set_net_variant(var)
     l1, v1 = eng.evaluate(pos)
     assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
     assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
