@@ -59,6 +59,10 @@ def main():
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
     ap.add_argument('--weights', default='', help='state_dict file (torch.save) instead of random init '
                                                   '(BASELINE config 3: a checkpoint trained by the loop)')
+    ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='N>1 end-of-run reductions: nccl (RCCL, one GPU per rank) or gloo (host; with '
+                         '--device, a rehearsal of the N-rank path on one GPU)')
+    ap.add_argument('--device', type=int, default=None, help='GPU of this rank (default LOCAL_RANK)')
     args = ap.parse_args()
 
     import numpy as np
@@ -67,12 +71,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
     dist = None
+    device = local if args.device is None else args.device
+    red_device = torch.device('cuda', device)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    device = local
+        torch.cuda.set_device(device)
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', device))
+        else:
+            dist.init_process_group('gloo')
+            red_device = torch.device('cpu')
 
     from minitchess_alphazero_amd.build import build
     if rank == 0 or world == 1:
@@ -123,7 +132,7 @@ def main():
             tot[k] += st[k]
     sync()
     dt = time.perf_counter() - t0
-    dt, tot = reduce_run(dt, tot, dist, torch.device('cuda', device))
+    dt, tot = reduce_run(dt, tot, dist, red_device)
     games = G * args.steps * world
     if rank != 0:
         if dist is not None:
