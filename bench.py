@@ -52,7 +52,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=0)
     ap.add_argument('--games', type=int, default=4096, help='parallel games per GPU (BASELINE config 2: 4096)')
     ap.add_argument('--sims', type=int, default=64, help='MCTS simulations per move (config 2: 64)')
-    ap.add_argument('--precision', default='f16x3', choices=['f16x3', 'fp32'])
+    ap.add_argument('--precision', default='f16x3', choices=['f16x3', 'f16f8', 'fp32'])
     ap.add_argument('--groups', type=int, default=1, help='game groups on separate HIP streams (mtaz_set_pipeline)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
@@ -145,11 +145,15 @@ def main():
     #    It runs on v_mfma_f32_16x16x32_f16, so the peak is the dense f16 MFMA rate; the 3
     #    split passes mean issued MFMA FLOP = 3x the trunk's algorithmic FLOP.
     #  fp32: k_conv3x3, 18 launches per wave; FLOP per launch = leaves x 2*30*256*2304.
-    f16x3 = st.get('net_precision', 0) == 1
+    prec = int(st.get('net_precision', 0))
+    f16x3 = prec in (1, 2)
     if f16x3:
         launches = tot['waves']
         flop_per_launch = FLOP_PER_EVAL * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
         kernel, peak = 'k_net_y (fused network, fp16x3 on MFMA 16x16x32 f16)', F16_MATRIX_PEAK_TFLOPS
+        if prec == 2:
+            kernel = ('k_net_z (fused network: Wh*Xh on MFMA 16x16x32 f16, cross terms on the block-scaled '
+                      'e4m3 MFMA 16x16x128)')
     else:
         launches = 18 * tot['waves']
         flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
@@ -175,7 +179,9 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'f16x3 (fp16 hi/lo split, fp32 accumulate; fp32-accurate)' if f16x3 else 'fp32',
+        'dtype': {1: 'f16x3 (fp16 hi/lo split, fp32 accumulate; fp32-accurate)',
+                  2: 'f16+e4m3 (fp16 hi/lo split; Wh*Xh in f16, cross terms in e4m3; fp32 accumulate; '
+                     'within 1e-5 of fp32)'}.get(prec, 'fp32'),
         'data': ('synthetic: self-play from STARTING_FEN, random-init weights (torch.manual_seed(0); Network())'
                  if not args.weights else f'synthetic: self-play from STARTING_FEN, trained checkpoint sha256 {weights_sha}'),
         'config': {'workload': (f'{G} parallel self-play games per GPU, {sims} sims/move, random-init policy net '

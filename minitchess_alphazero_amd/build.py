@@ -21,6 +21,7 @@ SOURCES = [
     ('mtaz_device.hip', ['-O3']),
     ('mtaz_net.hip', ['-O3']),
     ('mtaz_net16.hip', ['-O3']),
+    ('mtaz_net8.hip', ['-O3']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
     ('mtaz_wire.cpp', ['-O2']),
 ]

@@ -134,11 +134,20 @@ struct NetWeights {
   // weights, [2L+1] = max |folded bias| (L < 18); [36], [37] the same for the stem; [38] =
   // max |embedding|.  Each rounded up to float.
   const float* yrange;
+  // k_net_z (f16 + e4m3 cross terms): the split weights' hi and lo parts of convy, each scaled by
+  // a per-layer power of two and rounded to OCP e4m3, as the A operand of
+  // v_mfma_scale_f32_16x16x128_f8f6f4: [L 18][cotile 16][tap 9][chunk 2][part hi/lo][half 2]
+  // [lane 64][16 B]; lane l holds W[co = 16*cotile + (l&15)][ci = 128*chunk + 32*(l>>4) + j]
+  // (j = 16*half + byte) of that tap.  conv8_sc[2L + part] = the e8m0 scale that undoes the
+  // part's power of two (127 - a).
+  const uint4* conv8;
+  const int32_t* conv8_sc;
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
 constexpr size_t CONVX_U4_PER_LAYER = (size_t)8 * 144 * 2 * 64;  // 147,456 x 16 B = 2.36 MB
-enum NetPrecision { NET_FP32 = 0, NET_F16X3 = 1 };
+enum NetPrecision { NET_FP32 = 0, NET_F16X3 = 1, NET_F16F8 = 2 };
+constexpr size_t CONV8_U4_PER_LAYER = (size_t)16 * 9 * 2 * 2 * 2 * 64;   // 73,728 x 16 B = 1.18 MB
 constexpr int ERR_F16 = 512;   // activation exceeded the f16 range in the fp16x3 trunk
 
 struct NetBuffers {
@@ -177,6 +186,13 @@ void launch_net_y(const Dev& d, const NetWeights& w, const Pos* pos, const int32
                   float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
                   int variant);
 void launch_net_y_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
+// k_net_z (mtaz_net8.hip): the same fused network with the split's cross terms Wh*Xl + Wl*Xh on
+// the block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4), Wh*Xh on the f16 MFMA
+void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                  int variant);
+void launch_net_z_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
                           float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
 void launch_backup(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);

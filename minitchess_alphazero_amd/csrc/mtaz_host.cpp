@@ -467,6 +467,23 @@ double now_ms() {
 }
 }  // namespace
 
+// round to the nearest OCP e4m3fn value, ties to even (bias 7, subnormal step 2^-9; the
+// callers keep |v| < 448, larger magnitudes saturate to 448)
+static uint8_t to_e4m3(double v) {
+  const uint8_t sgn = v < 0 ? 0x80 : 0;
+  const double a = fabs(v);
+  if (a == 0) return sgn;
+  int e = ilogb(a);
+  if (e < -6) return sgn | (uint8_t)nearbyint(a * 512.0);   // 8 (= 0x08) is the least normal, 2^-6
+  double m = nearbyint(ldexp(a, 3 - e));                    // [8, 16]
+  if (m == 16) {
+    m = 8;
+    ++e;
+  }
+  if (e + 7 > 15 || (e + 7 == 15 && m - 8 >= 7)) return sgn | 0x7e;
+  return sgn | (uint8_t)(((e + 7) << 3) | (int)(m - 8));
+}
+
 struct mtaz_engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -865,6 +882,39 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             }
             sy[((((size_t)ct * 3 + kb) * 2 + part) * 64 + lane) * 8 + j] = v;
           }
+  // k_net_z: the split parts of wy (f16 hi / lo of W * 2^e) once more, each scaled by a per-layer
+  // power of two 2^a (largest |part| -> [128, 256)) and rounded to OCP e4m3, in the A-operand
+  // order of v_mfma_scale_f32_16x16x128_f8f6f4 (engine.h NetWeights::conv8); scale 127 - a.
+  std::vector<uint8_t> w8((size_t)CONV_LAYERS * CONV8_U4_PER_LAYER * 16);
+  std::vector<int32_t> sc8(2 * CONV_LAYERS + 4, 127);
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const _Float16* src = wy.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    // wy: [ct 16][kb 72][part 2][lane 64][8]; element (co, k) of part at lane (co&15) + 16*((k&31)>>3)
+    auto at = [&](int part, int co, int k) {
+      const int ct = co >> 4, kb = k >> 5, ln = (co & 15) + 16 * ((k & 31) >> 3);
+      return (double)src[((((size_t)ct * 72 + kb) * 2 + part) * 64 + ln) * 8 + (k & 7)];
+    };
+    int a[2];
+    for (int part = 0; part < 2; ++part) {
+      double mx = 0;
+      for (size_t i = 0; i < CONVX_U4_PER_LAYER * 8; ++i)
+        if (((i / 512) & 1) == (size_t)part) mx = std::max(mx, fabs((double)src[i]));
+      a[part] = mx > 0 ? 7 - ilogb(mx) : 0;
+      sc8[2 * L + part] = 127 - a[part];
+    }
+    uint8_t* dst = w8.data() + (size_t)L * CONV8_U4_PER_LAYER * 16;
+    for (int ct = 0; ct < 16; ++ct)
+      for (int t = 0; t < 9; ++t)
+        for (int c = 0; c < 2; ++c)
+          for (int part = 0; part < 2; ++part)
+            for (int half = 0; half < 2; ++half)
+              for (int lane = 0; lane < 64; ++lane)
+                for (int byte = 0; byte < 16; ++byte) {
+                  const int co = 16 * ct + (lane & 15), ci = 128 * c + 32 * (lane >> 4) + 16 * half + byte;
+                  const size_t u4 = (((((size_t)ct * 9 + t) * 2 + c) * 2 + part) * 2 + half) * 64 + lane;
+                  dst[u4 * 16 + byte] = to_e4m3(ldexp(at(part, co, t * 256 + ci), a[part]));
+                }
+  }
   // k_net_y output bounds (NetWeights::yrange): per conv the max over output channels of the
   // L1 norm of the folded weights and the max |folded bias|; the stem's; max |embedding|.
   std::vector<float> yr(2 * CONV_LAYERS + 3);
@@ -895,13 +945,16 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   if (!h->wyrange) ECHK(h->dalloc(&h->wyrange, yr.size()));
   HIPCHK(hipMemcpy(h->wyrange, yr.data(), yr.size() * 4, hipMemcpyHostToDevice));
   h->w.yrange = h->wyrange;
-  const size_t nx = wx.size() / 8, ns = sx.size() / 8, nsy = sy.size() / 8;
-  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, 2 * nx + ns + nsy));
+  const size_t nx = wx.size() / 8, ns = sx.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
+  const size_t nsc = (sc8.size() + 3) / 4;
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, 2 * nx + ns + nsy + n8 + nsc));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
   HIPCHK(hipMemcpy(h->wxbuf, wx.data(), nx * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + nx, sx.data(), ns * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + nx + ns, wy.data(), nx * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns, sy.data(), nsy * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy, w8.data(), n8 * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy + n8, sc8.data(), sc8.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx = h->wxbuf;
   h->w.convx_inv = h->wxinv;
@@ -909,13 +962,17 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.stemx_inv = h->wxinv + CONV_LAYERS;
   h->w.convy = h->wxbuf + nx + ns;
   h->w.stemy = h->wxbuf + 2 * nx + ns;
+  h->w.conv8 = h->wxbuf + 2 * nx + ns + nsy;
+  h->w.conv8_sc = reinterpret_cast<const int32_t*>(h->wxbuf + 2 * nx + ns + nsy + n8);
   h->weights_ok = true;
   return 0;
 }
 
 static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count, int max_b, int mode, float* logits,
                            float* values, hipEvent_t eb, hipEvent_t ee) {
-  if (h->precision == NET_F16X3) {
+  if (h->precision == NET_F16F8) {
+    launch_net_z(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee, h->variant);
+  } else if (h->precision == NET_F16X3) {
     launch_net_f16x3(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee, h->variant);
   } else {
     NetBuffers nb = h->nb;
@@ -953,7 +1010,10 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
   *ms_out = ms / iters;
   if (stamped && stamps_out) {
-    launch_net_f16x3_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
+    if (h->precision == NET_F16F8)
+      launch_net_z_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
+    else
+      launch_net_f16x3_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
     HIPCHK(hipMemcpyAsync(stamps_out, st, (size_t)nwg * NST * 8, hipMemcpyDeviceToHost, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1017,7 +1077,8 @@ extern "C" int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base) {
 }
 
 extern "C" int mtaz_set_precision(mtaz_engine* h, int precision) {
-  if (precision != NET_FP32 && precision != NET_F16X3) return set_err(MTAZ_E_FAIL, "precision must be 0 (fp32) or 1 (fp16x3)");
+  if (precision != NET_FP32 && precision != NET_F16X3 && precision != NET_F16F8)
+    return set_err(MTAZ_E_FAIL, "precision must be 0 (fp32), 1 (fp16x3) or 2 (f16 + e4m3 cross terms)");
   h->precision = precision;
   return 0;
 }

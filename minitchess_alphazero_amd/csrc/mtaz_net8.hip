@@ -1,0 +1,383 @@
+// k_net_z: the fused policy/value network (exp/policy.py:71-80 + the leaf priors of
+// exp/agent.py:67-69) with the fp16x3 split's cross terms on the block-scaled e4m3 MFMA.
+//
+// k_net_y computes each conv as Wh*Xh + Wh*Xl + Wl*Xh, three f16 MFMA passes.  The two cross
+// terms are 2^-11 of the product, so they need ~2^-11 relative precision only: k_net_z runs
+// them on v_mfma_scale_f32_16x16x128_f8f6f4 with OCP e4m3 operands (twice the f16 rate per
+// clock, MI355X_MICROARCH.md matrix-core table; 1.8-2.1x the f16 loop's FLOP/s on random data
+// in tools/probes/fp8_mfma_probe.hip, at a higher clock) and keeps Wh*Xh on
+// v_mfma_f32_16x16x32_f16: 2/3 of k_net_y's MFMA cycles for the same LDS and L2 bytes.
+// Emulated end to end (fp64 reference, 300 positions, seed-0 weights, tools/split_error.py) the
+// values move by 2e-6 and priors by 2e-8, against fp32's own 4e-8 / 5e-10: inside the 1e-5
+// parity bound, not bitwise k_net_y.
+//
+// Workgroup, tiling, stem, epilogue bound logic and heads are k_net_y's (mtaz_net16.hip).  The
+// LDS image keeps 4 B per activation: part 0 = Xh (f16, as k_net_y), part 1 = [Xl8 | Xh8], two
+// e4m3 copies (Xl = x - Xh and Xh itself), each in units of a per-layer power of two chosen
+// from the epilogue's rigorous output bound.  The residual is read back as Xh + Xl8 (precision
+// 2^-15 of x, part of the emulation above).
+//
+// K loop.  A conv's 72 steps s = (tap t, 128-channel chunk c, j): step s runs
+//   phase A: f16 MFMAs of k-block s (Wh x Xh, all 8 column tiles)
+//   phase B: e4m3 MFMAs (K = 128) of group G = s/2 = (t, c, term) on square tile pt = s&1:
+//            term 0: Wh8 x Xl8, term 1: Wl8 x Xh8
+// = 1024 MFMA cycles per step and SIMD.  Operands: Wh f16 fragments PD steps ahead, the e4m3
+// weight groups GD groups ahead (half a group per step), this step's e4m3 activation
+// fragments during phase A and the next step's f16 ones during phase B.
+//
+// VAR 2048: 8 waves (2 per SIMD), 32 output channels each.  With 4 waves the operands do not fit
+// the 256 arch VGPRs beside the address arithmetic (the compiler parks some in AGPRs and
+// shuffles them); with 8 waves each wave's weights halve and the accumulators take 64 AGPRs.
+#include "net_common.h"
+
+namespace mtaz {
+
+using namespace netc;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+constexpr int KBZ = 72;      // steps (= f16 k-blocks) per conv
+constexpr int GZ = 36;       // e4m3 groups per conv
+
+__device__ __forceinline__ i32x8 cat8(uint4 a, uint4 b) {
+  return (i32x8){(int)a.x, (int)a.y, (int)a.z, (int)a.w, (int)b.x, (int)b.y, (int)b.z, (int)b.w};
+}
+
+// 4 e4m3 bytes of {a, b, c, d} (round to nearest even, OCP e4m3fn)
+__device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d) {
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  return (uint32_t)r;
+}
+
+template <int VAR>
+constexpr int zWaves = (VAR & 2048) ? 8 : 4;
+
+template <bool STAMP, int VAR>
+__global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights W, const Pos* __restrict__ pos,
+                                                               const int32_t* __restrict__ count, int max_b, int mode,
+                                                               float* __restrict__ logits_out,
+                                                               float* __restrict__ values_out,
+                                                               unsigned long long* __restrict__ stamps) {
+  constexpr int NW = zWaves<VAR>, NT = 64 * NW, CT = 16 / NW;   // waves, threads, channel tiles per wave
+  __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
+  const int nb = count ? *count : max_b;
+  const int b0 = blockIdx.x * XB;
+  if (b0 >= nb) return;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, n = lane & 15, g = lane >> 4;
+  unsigned long long t_prev = 0, st_stem = 0, st_k = 0, st_epi = 0, st_heads = 0;
+  unsigned long long t_start = 0, r_start = 0;
+  if constexpr (STAMP) {
+    t_prev = t_start = __builtin_amdgcn_s_memtime();
+    r_start = __builtin_amdgcn_s_memrealtime();
+  }
+  auto stamp = [&](unsigned long long& acc) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - t_prev;
+      t_prev = t;
+    }
+  };
+
+  const int p1 = 16 + n;
+  const int ph0 = n / 5, pw0 = n % 5, ph1 = p1 / 5, pw1 = p1 % 5;
+  f32x4v acc[CT * 8];
+#pragma unroll
+  for (int i = 0; i < CT * 8; ++i) acc[i] = (f32x4v){0};
+  int overflow = 0;
+
+  // dynamic range (k_net_y): the image holds x * 2^-xs; mx_img = max of the current image
+  int xs = 0;
+  float mx_img = W.yrange[2 * CONV_LAYERS + 2];
+  float mx_blk = 0.f;
+  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMGB + AUXB - 16);
+  if (tid == 0) mxs[0] = mxs[1] = 0u;
+  int slot = 0;
+  // e4m3 exponent of the current image: Xh8 = e4m3(Xh * 2^sh), Xl8 = e4m3(Xl * 2^(sh + 11))
+  int sh = 0;
+
+  // Epilogue: y = ReLU(acc * 2^(xs - e - xo) + bias * 2^-xo) in stored units; part 0 <- f16(y),
+  // part 1 <- e4m3 copies of y - f16(y) and f16(y).  Conv A seeds conv B's accumulators with the
+  // block input Xh + Xl8 (conv B's units), read before its own store.
+  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next, float bound) {
+    constexpr bool conv_a = decltype(conv_a_t)::value;
+    const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
+    const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
+    const float sseed = __builtin_ldexpf(s_next, xs - xo);
+    // stored values are <= bound * 2^-xo =: bs; sh_new = 7 - ilogb(bs) keeps e4m3(Xh * 2^sh) < 256
+    // (clamped so that 2^(sh + 11) stays a normal float)
+    const float bs = __builtin_ldexpf(bound, -xo);
+    const int eb = bs > 0.f ? (int)((__float_as_uint(bs) >> 23) & 0xffu) - 127 : -126;
+    int sh_new = bs < __builtin_inff() ? 7 - eb : 0;
+    sh_new = sh_new > 60 ? 60 : sh_new < -60 ? -60 : sh_new;
+    const float hs = __builtin_ldexpf(1.f, sh_new), ls = __builtin_ldexpf(1.f, sh_new + 11);
+    const float lo_in = __builtin_ldexpf(1.f, -(sh + 11));   // Xl8 units of the image being read
+    float ymax = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int co0 = 16 * CT * wave + 16 * ct + 4 * g;
+      const float4 bu = *reinterpret_cast<const float4*>(bias + co0);
+      const float4 bv = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int bb = t >> 1, pt = t & 1;
+        f32x4v& a = acc[ct * 8 + t];
+        if (pt == 0 || p1 < 30) {
+          const int p = pt ? p1 : n;
+          const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1);
+          const int al8 = ioff(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
+          const int ah8 = ioff(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
+          float y[4];
+          y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
+          y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
+          y[2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv.z), 0.f);
+          y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
+          ymax = fmaxf(fmaxf(ymax, fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
+          if constexpr (conv_a) {
+            const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
+            const int xl = *reinterpret_cast<const int*>(smem + al8);
+            const float ls_in = lo_in * sseed;
+            a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in);
+            a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in);
+            a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in);
+            a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in);
+          } else {
+            a = (f32x4v){0};
+          }
+          f16x4 yh;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
+          float h[4], l[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            h[j] = (float)yh[j];
+            l[j] = (y[j] - h[j]) * ls;   // exact difference, power-of-two scale
+            h[j] *= hs;
+          }
+          *reinterpret_cast<f16x4*>(smem + ah) = yh;
+          *reinterpret_cast<uint32_t*>(smem + al8) = pk_fp8x4(l[0], l[1], l[2], l[3]);
+          *reinterpret_cast<uint32_t*>(smem + ah8) = pk_fp8x4(h[0], h[1], h[2], h[3]);
+        } else {
+          a = (f32x4v){0};
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o, 64));
+    if (lane == 0) atomicMax(&mxs[slot], __float_as_uint(ymax));
+    if (tid == 0) mxs[slot ^ 1] = 0u;
+    xs = xo;
+    sh = sh_new;
+    __syncthreads();
+    mx_img = __builtin_ldexpf(__uint_as_float(mxs[slot]), xo);
+    slot ^= 1;
+    if (!__builtin_isfinite(mx_img)) overflow = 1;
+  };
+
+  // ---------------- stem: conv3x3 8->256 in f16x3 (k_net_y's), K = 3 k-blocks -------------
+  // (stem_input zeroes both parts' zero rows, which covers [Xl8 | Xh8] of the zero row)
+  char* simg = smem + IMGB;
+  stem_input<NT>(smem, simg, pos, b0, nb, W, tid);
+  __syncthreads();
+  {
+    const uint4* Ws = W.stemy + (size_t)(CT * wave) * 3 * 128 + lane;
+    for (int kb = 0; kb < 3; ++kb) {
+      f16x8 SA[2 * CT], SB[16];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        SA[2 * c] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128]);
+        SA[2 * c + 1] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128 + 64]);
+      }
+      const int tap = 4 * kb + g;
+      const int r0 = tap < 9 ? src_row(n, ph0, pw0, tap) : ZROW;
+      const int r1 = tap < 9 ? src_row(p1, ph1, pw1, tap) : ZROW;
+#pragma unroll
+      for (int part = 0; part < 2; ++part)
+#pragma unroll
+        for (int bb = 0; bb < XB; ++bb) {
+          SB[part * 8 + 2 * bb] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r0) * 16);
+          SB[part * 8 + 2 * bb + 1] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r1) * 16);
+        }
+#pragma unroll
+      for (int ps = 0; ps < 3; ++ps) {
+        const int wp = ps == 2 ? 1 : 0, xp = ps == 1 ? 1 : 0;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            acc[ct * 8 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(SA[2 * ct + wp], SB[xp * 8 + t], acc[ct * 8 + t], 0, 0, 0);
+      }
+    }
+  }
+  epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f,
+           __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mx_img, W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f);
+  stamp(st_stem);
+
+  // ---------------- residual trunk ----------------------------------------------------------
+  constexpr int PD = NW == 8 ? 1 : 2, RA = PD + 1, GD = 1, RG = 2;
+  constexpr int U = RA == 2 ? 4 : 12;
+  static_assert(KBZ % U == 0 && U % RA == 0 && (U / 2) % RG == 0 && RG > GD, "rings");
+  f16x8 A16[RA][CT], B16[8];
+  i32x8 A8[RG][CT], B8[4];
+  const int n_ = n, p1_ = p1, ph0_ = ph0, pw0_ = pw0, ph1_ = ph1, pw1_ = pw1, g_ = g;
+  const uint4* Wh = W.convy + (size_t)(CT * wave) * KBZ * 128 + lane;          // hi parts of convy
+  const uint4* W8 = W.conv8 + (size_t)(CT * wave) * GZ * 128 + lane;
+  const int32_t* sc8 = W.conv8_sc;
+
+  // Wh fragments of step (k-block) KB, the wave's channel tiles
+#define Z_LOAD_A16(S, KB)                                                             \
+  {                                                                                   \
+    const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
+    _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_)                                 \
+      S[c_] = __builtin_bit_cast(f16x8, Wh[((size_t)c_ * KBZ + kk_) * 128]);          \
+  }
+  // e4m3 weight fragments of group GR (tap, chunk, term), channel tiles [C0, C0 + CT/2)
+#define Z_LOAD_A8(S, GR, C0)                                                          \
+  {                                                                                   \
+    const int gg_ = (GR) < GZ ? (GR) : GZ - 1;                                        \
+    _Pragma("unroll") for (int c_ = (C0); c_ < (C0) + CT / 2; ++c_) {                 \
+      const uint4* p_ = W8 + ((size_t)c_ * GZ + gg_) * 128;                           \
+      S[c_] = cat8(p_[0], p_[64]);                                                    \
+    }                                                                                 \
+  }
+  // Xh (f16) fragments of step KB for both square tiles: S16[2 * board + tile]
+#define Z_LOAD_B16(S16, KB)                                                           \
+  {                                                                                   \
+    const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
+    const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
+    const int r0_ = src_row(n, ph0, pw0, tap_), r1_ = src_row(p1, ph1, pw1, tap_);    \
+    const int o0_ = r0_ * RB + ((ch_ ^ (r0_ & 15)) << 4);                             \
+    const int o1_ = r1_ * RB + ((ch_ ^ (r1_ & 15)) << 4);                             \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
+      const char* base_ = smem + bb_ * IROWS * RB;                                    \
+      S16[2 * bb_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                   \
+      S16[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);               \
+    }                                                                                 \
+  }
+  // e4m3 fragments of step KB's group on square tile KB & 1 (Xl8 for term 0, Xh8 for term 1):
+  // lane (g, n) takes the 32 channels [128 c + 32 g, +32) of its source square
+#define Z_LOAD_B8(S8, KB)                                                             \
+  {                                                                                   \
+    const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
+    const int tap_ = kk_ >> 3, term_ = (kk_ >> 1) & 1, cc_ = (kk_ >> 2) & 1;          \
+    const int r_ = (kk_ & 1) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_); \
+    const int q0_ = 16 * term_ + 8 * cc_ + 2 * g;                                     \
+    const int f0_ = r_ * RB + ((q0_ ^ (r_ & 15)) << 4);                               \
+    const int f1_ = r_ * RB + (((q0_ + 1) ^ (r_ & 15)) << 4);                         \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
+      const char* base_ = smem + PARTB + bb_ * IROWS * RB;                            \
+      S8[bb_] = cat8(*reinterpret_cast<const uint4*>(base_ + f0_),                   \
+                     *reinterpret_cast<const uint4*>(base_ + f1_));                  \
+    }                                                                                 \
+  }
+
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    // the lane's square coordinates, opaque to the compiler per layer: the LDS offsets of the
+    // 72 steps are recomputed in the loop (a few VALU each) instead of being hoisted out of the
+    // layer loop into ~150 VGPRs
+    int n = n_, p1 = p1_, ph0 = ph0_, pw0 = pw0_, ph1 = ph1_, pw1 = pw1_, g = g_;
+    asm volatile("" : "+v"(n), "+v"(p1), "+v"(ph0), "+v"(pw0), "+v"(ph1), "+v"(pw1), "+v"(g));
+    const int sa_h = sc8[2 * L], sa_l = sc8[2 * L + 1];
+    const int sb_l = 127 - (sh + 11), sb_h = 127 - sh;   // the input image's e4m3 units
+#pragma unroll
+    for (int p = 0; p < PD; ++p) Z_LOAD_A16(A16[p], p);
+#pragma unroll
+    for (int p = 0; p < GD; ++p) {
+      Z_LOAD_A8(A8[p], p, 0)
+      Z_LOAD_A8(A8[p], p, CT / 2)
+    }
+    Z_LOAD_B16(B16, 0);
+#pragma unroll 1
+    for (int s0 = 0; s0 < KBZ; s0 += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int s = s0 + u;
+        // phase A: Wh x Xh of k-block s on every column tile; meanwhile this step's e4m3
+        // activation fragments and the Wh fragments PD steps ahead
+        __builtin_amdgcn_sched_barrier(0);
+        Z_LOAD_B8(B8, s);
+        Z_LOAD_A16(A16[(u + PD) % RA], s + PD);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            acc[ct * 8 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A16[u % RA][ct], B16[t], acc[ct * 8 + t], 0, 0, 0);
+        // phase B: group s/2 on square tile s&1; meanwhile the next step's Xh fragments and half
+        // of the e4m3 weight group GD groups ahead
+        __builtin_amdgcn_sched_barrier(0);
+        Z_LOAD_B16(B16, s + 1);
+        Z_LOAD_A8(A8[((u >> 1) + GD) % RG], (s >> 1) + GD, (CT / 2) * (u & 1));
+        const int pt = u & 1;
+        const bool term = (u >> 1) & 1;
+        const int sa = term ? sa_l : sa_h, sb = term ? sb_h : sb_l;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int bb = 0; bb < XB; ++bb)
+            acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 0, 0, 0, sa, 0, sb);
+      }
+    }
+    stamp(st_k);
+    Wh += CONVX_U4_PER_LAYER;
+    W8 += CONV8_U4_PER_LAYER;
+    __syncthreads();
+    if ((L & 1) == 0) {
+      const float bound = __builtin_fmaf(W.yrange[2 * L], mx_img, W.yrange[2 * L + 1]) * 1.0009765625f;
+      mx_blk = mx_img;
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bound);
+    } else {
+      const float bound = (__builtin_fmaf(W.yrange[2 * L], mx_img, W.yrange[2 * L + 1]) + mx_blk) * 1.0009765625f;
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bound);
+    }
+    stamp(st_epi);
+  }
+#undef Z_LOAD_A16
+#undef Z_LOAD_A8
+#undef Z_LOAD_B16
+#undef Z_LOAD_B8
+  if (overflow) atomicOr(D.pr.err, ERR_F16);
+
+  heads_reduce<NT, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs), __builtin_ldexpf(1.f, -(sh + 11)));
+  stamp(st_heads);
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      stamps[blockIdx.x * 6 + 0] = st_stem;
+      stamps[blockIdx.x * 6 + 1] = st_k;
+      stamps[blockIdx.x * 6 + 2] = st_epi;
+      stamps[blockIdx.x * 6 + 3] = st_heads;
+      stamps[blockIdx.x * 6 + 4] = __builtin_amdgcn_s_memtime() - t_start;
+      stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
+    }
+  }
+  heads_out(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
+}
+
+template <bool S>
+static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
+                     const int32_t* count, int max_b, int mode, float* logits, float* values,
+                     unsigned long long* stamps) {
+  if (var & 2048)
+    hipLaunchKernelGGL((k_net_z<S, 2048>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else
+    hipLaunchKernelGGL((k_net_z<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+}
+
+void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                  int variant) {
+  if (max_b <= 0) return;
+  if (ev_begin) (void)hipEventRecord(ev_begin, s);
+  launch_z<false>(variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode, logits_out, values_out,
+                  nullptr);
+  if (ev_end) (void)hipEventRecord(ev_end, s);
+}
+
+void launch_net_z_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
+                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant) {
+  if (n <= 0) return;
+  launch_z<true>(variant, dim3((n + XB - 1) / XB), s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS, logits_out,
+                 values_out, stamps);
+}
+
+}  // namespace mtaz

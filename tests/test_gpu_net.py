@@ -27,7 +27,7 @@ def _softmax(x):
 # f16x3-x* = k_net_x (32x32x16 MFMA, variant bit 512) and its schedules; fp32 = fp32 MFMA path
 NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4), 'f16x3-y128': ('f16x3', 128),
                'f16x3-y8': ('f16x3', 8), 'f16x3-x': ('f16x3', 512), 'f16x3-y2048': ('f16x3', 2048),
-               'f16x3-y6144': ('f16x3', 6144)}
+               'f16x3-y6144': ('f16x3', 6144), 'f16f8': ('f16f8', 0), 'f16f8-w8': ('f16f8', 2048)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))

@@ -28,7 +28,8 @@ def main():
     ap.add_argument('--n', type=int, default=4096)
     ap.add_argument('--iters', type=int, default=10)
     ap.add_argument('--rounds', type=int, default=3)
-    ap.add_argument('--variants', default='0')
+    ap.add_argument('--variants', default='0', help='comma list of VARIANT or PRECISION:VARIANT '
+                                                   '(e.g. f16x3:0,f16f8:0,f16f8:2048)')
     ap.add_argument('--precision', default='f16x3')
     args = ap.parse_args()
     import torch
@@ -45,12 +46,14 @@ def main():
     eng.set_precision(args.precision)
     d = torch.from_numpy(pos.view(np.int32)).cuda()
     torch.cuda.synchronize()
-    variants = [int(v) for v in args.variants.split(',')]
+    variants = [v if ':' in v else f'{args.precision}:{v}' for v in args.variants.split(',')]
     nwg = (args.n + 3) // 4
     res = {v: {'ms': [], 'cycles': [], 'ghz': [], 'shares': []} for v in variants}
     for _ in range(args.rounds):
         for v in variants:
-            _lib.check(eng.L.mtaz_set_net_variant(eng.h, v))
+            prec, var = v.split(':')
+            eng.set_precision(prec)
+            _lib.check(eng.L.mtaz_set_net_variant(eng.h, int(var)))
             ms = ctypes.c_float()
             st = np.zeros(nwg * 6, np.uint64)
             _lib.check(eng.L.mtaz_net_time(eng.h, ctypes.c_void_p(d.data_ptr()), args.n, args.iters, 1,
@@ -63,7 +66,7 @@ def main():
     for v in variants:
         r = res[v]
         ms = float(np.median(r['ms']))
-        out = {'variant': v, 'n': args.n, 'precision': args.precision, 'ms_median': ms, 'ms_all': r['ms'],
+        out = {'variant': v, 'n': args.n, 'ms_median': ms, 'ms_all': r['ms'],
                'tflops_algorithmic': FLOP_PER_EVAL * args.n / (ms * 1e-3) / 1e12,
                'wg_cycles': float(np.median(r['cycles'])), 'clock_ghz_stamped': float(np.median(r['ghz'])),
                'shares': dict(zip(['stem', 'conv_kloop', 'conv_epilogue', 'heads'],
