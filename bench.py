@@ -52,7 +52,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=0)
     ap.add_argument('--games', type=int, default=4096, help='parallel games per GPU (BASELINE config 2: 4096)')
     ap.add_argument('--sims', type=int, default=64, help='MCTS simulations per move (config 2: 64)')
-    ap.add_argument('--precision', default='f16x3', choices=['f16x3', 'f16f8', 'fp32'])
+    ap.add_argument('--precision', default='f16f8', choices=['f16x3', 'f16f8', 'fp32'])
     ap.add_argument('--groups', type=int, default=1, help='game groups on separate HIP streams (mtaz_set_pipeline)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
@@ -140,7 +140,9 @@ def main():
         return
 
     # roofline of the dominant kernel, timed with HIP events on the engine's stream:
-    #  fp16x3 (default): k_net_y, ONE launch per simulation wave = the whole network on the
+    #  f16f8 (default): k_net_z, as k_net_y below with the split's two cross terms on the
+    #    block-scaled e4m3 MFMA (16x16x128); algorithmic FLOP as below.
+    #  f16x3: k_net_y, ONE launch per simulation wave = the whole network on the
     #    wave's leaves; algorithmic FLOP per launch = leaves x 638,245,892.
     #    It runs on v_mfma_f32_16x16x32_f16, so the peak is the dense f16 MFMA rate; the 3
     #    split passes mean issued MFMA FLOP = 3x the trunk's algorithmic FLOP.
@@ -158,13 +160,14 @@ def main():
         launches = 18 * tot['waves']
         flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
         kernel, peak = 'k_conv3x3 (fp32 MFMA 32x32x2)', FP32_MATRIX_PEAK_TFLOPS
+    passes_eq = {1: 3.0, 2: 2.0}.get(prec, 1.0)
     conv_ms_avg = tot['trunk_ms'] / launches if launches else float('nan')
     achieved = flop_per_launch / (conv_ms_avg * 1e-3) / 1e12
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get('games') == args.games and tj.get('sims') == args.sims:
+            if tj.get('games') == args.games and tj.get('sims') == args.sims and kernel.startswith(tj.get('kernel', '?')):
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
@@ -199,11 +202,13 @@ def main():
         'roofline': {'bound': 'mfma', 'kernel': kernel, 'achieved': achieved,
                      'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
                      'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch,
-                     'mfma_passes': 3 if f16x3 else 1,
-                     # the f16 MFMA FLOP the split actually issues (3 passes per algorithmic FLOP),
-                     # over the same dense f16 peak: the MFMA pipe's utilisation
-                     'issued_achieved': achieved * (3 if f16x3 else 1),
-                     'issued_frac': achieved * (3 if f16x3 else 1) / peak},
+                     'mfma_passes': {1: 'f16 x3', 2: 'f16 x1 + e4m3 x2'}.get(prec, 'f32 x1'),
+                     # the MFMA work the split actually issues, in dense-f16 equivalents (an e4m3
+                     # MFMA of the block-scaled form runs at twice the f16 rate: 3 passes for
+                     # f16x3, 1 + 2/2 for f16+e4m3), over the same dense f16 peak: the MFMA
+                     # pipes' utilisation
+                     'issued_achieved': achieved * passes_eq,
+                     'issued_frac': achieved * passes_eq / peak},
         # secondary roofline: the tree kernel k_select, HBM/latency-bound; algorithmic
         # bytes per simulation = SURVEY's estimate (path nodes: header + k edge reads + edge update,
         # leaf insert, hash probe, NN input) at k ~ 7.5, depth ~ 2

@@ -495,7 +495,7 @@ struct mtaz_engine {
   NetWeights w{};
   NetBuffers nb{};
   bool weights_ok = false;
-  int precision = NET_F16X3;
+  int precision = NET_F16F8;   // k_net_z; NET_F16X3 = k_net_y (fp32-accurate to ~1e-8)
   int variant = 0;   // fp16x3 network kernel variant (0 = product k_net_y; NET_VAR_X = k_net_x)
   uint4* wxbuf = nullptr;
   float* wxinv = nullptr;

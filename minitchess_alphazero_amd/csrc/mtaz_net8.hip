@@ -14,7 +14,7 @@
 // Workgroup, tiling, stem, epilogue bound logic and heads are k_net_y's (mtaz_net16.hip).  The
 // LDS image keeps 4 B per activation: part 0 = Xh (f16, as k_net_y), part 1 = [Xl8 | Xh8], two
 // e4m3 copies (Xl = x - Xh and Xh itself), each in units of a per-layer power of two chosen
-// from the epilogue's rigorous output bound.  The residual is read back as Xh + Xl8 (precision
+// per board from the epilogue's rigorous output bound.  The residual is read back as Xh + Xl8 (precision
 // 2^-15 of x, part of the emulation above).
 //
 // K loop.  A conv's 72 steps s = (tap t, 128-channel chunk c, j): step s runs
@@ -25,9 +25,10 @@
 // weight groups GD groups ahead (half a group per step), this step's e4m3 activation
 // fragments during phase A and the next step's f16 ones during phase B.
 //
-// VAR 2048: 8 waves (2 per SIMD), 32 output channels each.  With 4 waves the operands do not fit
-// the 256 arch VGPRs beside the address arithmetic (the compiler parks some in AGPRs and
-// shuffles them); with 8 waves each wave's weights halve and the accumulators take 64 AGPRs.
+// Waves: 8 (2 per SIMD), 32 output channels each.  VAR 2048 = 4 waves of 64 channels, k_net_y's
+// layout; there the operands do not fit the 256 arch VGPRs beside the address arithmetic (the
+// compiler parks some in AGPRs and shuffles them), with 8 waves each wave's weights halve and
+// the accumulators take 64 AGPRs.  VAR 4096: prefetch one step / one e4m3 group further ahead.
 #include "net_common.h"
 
 namespace mtaz {
@@ -50,7 +51,7 @@ __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d)
 }
 
 template <int VAR>
-constexpr int zWaves = (VAR & 2048) ? 8 : 4;
+constexpr int zWaves = (VAR & 2048) ? 4 : 8;
 
 template <bool STAMP, int VAR>
 __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights W, const Pos* __restrict__ pos,
@@ -86,33 +87,46 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   for (int i = 0; i < CT * 8; ++i) acc[i] = (f32x4v){0};
   int overflow = 0;
 
-  // dynamic range (k_net_y): the image holds x * 2^-xs; mx_img = max of the current image
+  // dynamic range (k_net_y): the image holds x * 2^-xs, one xs per workgroup (0 for any ordinary
+  // net).  mxb[bb] = max of board bb's current image, measured by the epilogue that stored it.
   int xs = 0;
-  float mx_img = W.yrange[2 * CONV_LAYERS + 2];
-  float mx_blk = 0.f;
-  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMGB + AUXB - 16);
-  if (tid == 0) mxs[0] = mxs[1] = 0u;
+  float mxb[XB], mxblk[XB];
+#pragma unroll
+  for (int bb = 0; bb < XB; ++bb) mxb[bb] = W.yrange[2 * CONV_LAYERS + 2], mxblk[bb] = 0.f;
+  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMGB + AUXB - 4 * 2 * XB);   // [slot 2][board]
+  if (tid < 2 * XB) mxs[tid] = 0u;
   int slot = 0;
-  // e4m3 exponent of the current image: Xh8 = e4m3(Xh * 2^sh), Xl8 = e4m3(Xl * 2^(sh + 11))
-  int sh = 0;
+  // e4m3 exponents of board bb's current image: Xh8 = e4m3(Xh * 2^sh[bb]),
+  // Xl8 = e4m3(Xl * 2^(sh[bb] + 11)).  Per board (from the board's own bound), so a board's
+  // results do not depend on the boards it shares a workgroup with.
+  int sh[XB] = {0, 0, 0, 0};
 
   // Epilogue: y = ReLU(acc * 2^(xs - e - xo) + bias * 2^-xo) in stored units; part 0 <- f16(y),
   // part 1 <- e4m3 copies of y - f16(y) and f16(y).  Conv A seeds conv B's accumulators with the
   // block input Xh + Xl8 (conv B's units), read before its own store.
-  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next, float bound) {
+  // boundb[bb]: rigorous bound on board bb's outputs (true units); the workgroup's xo follows
+  // their max, as k_net_y's
+  auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next, const float* boundb) {
     constexpr bool conv_a = decltype(conv_a_t)::value;
+    const float bound = fmaxf(fmaxf(boundb[0], boundb[1]), fmaxf(boundb[2], boundb[3]));
     const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
     const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
     const float sseed = __builtin_ldexpf(s_next, xs - xo);
-    // stored values are <= bound * 2^-xo =: bs; sh_new = 7 - ilogb(bs) keeps e4m3(Xh * 2^sh) < 256
-    // (clamped so that 2^(sh + 11) stays a normal float)
-    const float bs = __builtin_ldexpf(bound, -xo);
-    const int eb = bs > 0.f ? (int)((__float_as_uint(bs) >> 23) & 0xffu) - 127 : -126;
-    int sh_new = bs < __builtin_inff() ? 7 - eb : 0;
-    sh_new = sh_new > 60 ? 60 : sh_new < -60 ? -60 : sh_new;
-    const float hs = __builtin_ldexpf(1.f, sh_new), ls = __builtin_ldexpf(1.f, sh_new + 11);
-    const float lo_in = __builtin_ldexpf(1.f, -(sh + 11));   // Xl8 units of the image being read
-    float ymax = 0.f;
+    // board bb's stored values are <= boundb[bb] * 2^-xo =: bs; sh_new = 7 - ilogb(bs) keeps
+    // e4m3(Xh * 2^sh) < 256 (clamped so that 2^(sh + 11) stays a normal float)
+    int sh_new[XB];
+    float hs[XB], ls[XB], ls_in[XB];
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) {
+      const float bs = __builtin_ldexpf(boundb[bb], -xo);
+      const int eb = bs > 0.f ? (int)((__float_as_uint(bs) >> 23) & 0xffu) - 127 : -126;
+      int e = bs < __builtin_inff() ? 7 - eb : 0;
+      sh_new[bb] = e > 60 ? 60 : e < -60 ? -60 : e;
+      hs[bb] = __builtin_ldexpf(1.f, sh_new[bb]);
+      ls[bb] = __builtin_ldexpf(1.f, sh_new[bb] + 11);
+      ls_in[bb] = __builtin_ldexpf(sseed, -(sh[bb] + 11));   // Xl8 units of the image being read
+    }
+    float ymax[XB] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int co0 = 16 * CT * wave + 16 * ct + 4 * g;
@@ -132,15 +146,14 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
           y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
           y[2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv.z), 0.f);
           y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
-          ymax = fmaxf(fmaxf(ymax, fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
+          ymax[bb] = fmaxf(fmaxf(ymax[bb], fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
           if constexpr (conv_a) {
             const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
             const int xl = *reinterpret_cast<const int*>(smem + al8);
-            const float ls_in = lo_in * sseed;
-            a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in);
-            a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in);
-            a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in);
-            a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in);
+            a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[bb]);
+            a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[bb]);
+            a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[bb]);
+            a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[bb]);
           } else {
             a = (f32x4v){0};
           }
@@ -151,8 +164,8 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             h[j] = (float)yh[j];
-            l[j] = (y[j] - h[j]) * ls;   // exact difference, power-of-two scale
-            h[j] *= hs;
+            l[j] = (y[j] - h[j]) * ls[bb];   // exact difference, power-of-two scale
+            h[j] *= hs[bb];
           }
           *reinterpret_cast<f16x4*>(smem + ah) = yh;
           *reinterpret_cast<uint32_t*>(smem + al8) = pk_fp8x4(l[0], l[1], l[2], l[3]);
@@ -162,16 +175,27 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         }
       }
     }
+    // per-board maxima of the new image (y >= 0: float bits order as values)
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o, 64));
-    if (lane == 0) atomicMax(&mxs[slot], __float_as_uint(ymax));
-    if (tid == 0) mxs[slot ^ 1] = 0u;
+    for (int bb = 0; bb < XB; ++bb) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) ymax[bb] = fmaxf(ymax[bb], __shfl_xor(ymax[bb], o, 64));
+    }
+    if (lane < XB) {
+      const float m = lane == 0 ? ymax[0] : lane == 1 ? ymax[1] : lane == 2 ? ymax[2] : ymax[3];
+      atomicMax(&mxs[slot * XB + lane], __float_as_uint(m));
+    }
+    if (tid < XB) mxs[(slot ^ 1) * XB + tid] = 0u;   // every wave read them before this epilogue's barrier
     xs = xo;
-    sh = sh_new;
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) sh[bb] = sh_new[bb];
     __syncthreads();
-    mx_img = __builtin_ldexpf(__uint_as_float(mxs[slot]), xo);
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) {
+      mxb[bb] = __builtin_ldexpf(__uint_as_float(mxs[slot * XB + bb]), xo);
+      if (!__builtin_isfinite(mxb[bb])) overflow = 1;
+    }
     slot ^= 1;
-    if (!__builtin_isfinite(mx_img)) overflow = 1;
   };
 
   // ---------------- stem: conv3x3 8->256 in f16x3 (k_net_y's), K = 3 k-blocks -------------
@@ -209,13 +233,19 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
       }
     }
   }
-  epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f,
-           __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mx_img, W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f);
+  {
+    float bnd[XB];
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb)
+      bnd[bb] = __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mxb[bb], W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f;
+    epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f, bnd);
+  }
   stamp(st_stem);
 
   // ---------------- residual trunk ----------------------------------------------------------
-  constexpr int PD = NW == 8 ? 1 : 2, RA = PD + 1, GD = 1, RG = 2;
-  constexpr int U = RA == 2 ? 4 : 12;
+  constexpr bool DEEP = (VAR & 4096) != 0;
+  constexpr int PD = (NW == 8 ? 1 : 2) + (DEEP ? 1 : 0), RA = PD + 1, GD = DEEP ? 2 : 1, RG = GD + 1;
+  constexpr int U = (RA == 2 && RG == 2) ? 4 : 12;
   static_assert(KBZ % U == 0 && U % RA == 0 && (U / 2) % RG == 0 && RG > GD, "rings");
   f16x8 A16[RA][CT], B16[8];
   i32x8 A8[RG][CT], B8[4];
@@ -262,13 +292,12 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     const int tap_ = kk_ >> 3, term_ = (kk_ >> 1) & 1, cc_ = (kk_ >> 2) & 1;          \
     const int r_ = (kk_ & 1) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_); \
     const int q0_ = 16 * term_ + 8 * cc_ + 2 * g;                                     \
-    const int f0_ = r_ * RB + ((q0_ ^ (r_ & 15)) << 4);                               \
-    const int f1_ = r_ * RB + (((q0_ + 1) ^ (r_ & 15)) << 4);                         \
-    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
-      const char* base_ = smem + PARTB + bb_ * IROWS * RB;                            \
-      S8[bb_] = cat8(*reinterpret_cast<const uint4*>(base_ + f0_),                   \
-                     *reinterpret_cast<const uint4*>(base_ + f1_));                  \
-    }                                                                                 \
+    /* part-1 row base once, so that the boards' offsets (< 64 KB) fit the ds_read immediate */ \
+    const char* p0_ = smem + PARTB + r_ * RB + ((q0_ ^ (r_ & 15)) << 4);              \
+    const char* p1_ = smem + PARTB + r_ * RB + (((q0_ + 1) ^ (r_ & 15)) << 4);        \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                              \
+      S8[bb_] = cat8(*reinterpret_cast<const uint4*>(p0_ + bb_ * IROWS * RB),        \
+                     *reinterpret_cast<const uint4*>(p1_ + bb_ * IROWS * RB));       \
   }
 
   for (int L = 0; L < CONV_LAYERS; ++L) {
@@ -278,7 +307,9 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     int n = n_, p1 = p1_, ph0 = ph0_, pw0 = pw0_, ph1 = ph1_, pw1 = pw1_, g = g_;
     asm volatile("" : "+v"(n), "+v"(p1), "+v"(ph0), "+v"(pw0), "+v"(ph1), "+v"(pw1), "+v"(g));
     const int sa_h = sc8[2 * L], sa_l = sc8[2 * L + 1];
-    const int sb_l = 127 - (sh + 11), sb_h = 127 - sh;   // the input image's e4m3 units
+    int sb_l[XB], sb_h[XB];   // the input image's e4m3 units, per board
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) sb_l[bb] = 127 - (sh[bb] + 11), sb_h[bb] = 127 - sh[bb];
 #pragma unroll
     for (int p = 0; p < PD; ++p) Z_LOAD_A16(A16[p], p);
 #pragma unroll
@@ -309,26 +340,33 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         Z_LOAD_A8(A8[((u >> 1) + GD) % RG], (s >> 1) + GD, (CT / 2) * (u & 1));
         const int pt = u & 1;
         const bool term = (u >> 1) & 1;
-        const int sa = term ? sa_l : sa_h, sb = term ? sb_h : sb_l;
+        const int sa = term ? sa_l : sa_h;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
           for (int bb = 0; bb < XB; ++bb)
             acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 0, 0, 0, sa, 0, sb);
+                A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 0, 0, 0, sa, 0,
+                term ? sb_h[bb] : sb_l[bb]);
       }
     }
-    stamp(st_k);
     Wh += CONVX_U4_PER_LAYER;
     W8 += CONV8_U4_PER_LAYER;
     __syncthreads();
+    stamp(st_k);   // (k_net_z: the K-loop share includes the wait for the workgroup's slowest wave)
+    float bnd[XB];
     if ((L & 1) == 0) {
-      const float bound = __builtin_fmaf(W.yrange[2 * L], mx_img, W.yrange[2 * L + 1]) * 1.0009765625f;
-      mx_blk = mx_img;
-      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bound);
+#pragma unroll
+      for (int bb = 0; bb < XB; ++bb) {
+        bnd[bb] = __builtin_fmaf(W.yrange[2 * L], mxb[bb], W.yrange[2 * L + 1]) * 1.0009765625f;
+        mxblk[bb] = mxb[bb];
+      }
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bnd);
     } else {
-      const float bound = (__builtin_fmaf(W.yrange[2 * L], mx_img, W.yrange[2 * L + 1]) + mx_blk) * 1.0009765625f;
-      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bound);
+#pragma unroll
+      for (int bb = 0; bb < XB; ++bb)
+        bnd[bb] = (__builtin_fmaf(W.yrange[2 * L], mxb[bb], W.yrange[2 * L + 1]) + mxblk[bb]) * 1.0009765625f;
+      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bnd);
     }
     stamp(st_epi);
   }
@@ -338,7 +376,9 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #undef Z_LOAD_B8
   if (overflow) atomicOr(D.pr.err, ERR_F16);
 
-  heads_reduce<NT, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs), __builtin_ldexpf(1.f, -(sh + 11)));
+  heads_reduce<NT, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
+                         make_float4(__builtin_ldexpf(1.f, -(sh[0] + 11)), __builtin_ldexpf(1.f, -(sh[1] + 11)),
+                                     __builtin_ldexpf(1.f, -(sh[2] + 11)), __builtin_ldexpf(1.f, -(sh[3] + 11))));
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
@@ -358,9 +398,11 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
   if (var & 2048)
-    hipLaunchKernelGGL((k_net_z<S, 2048>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+    hipLaunchKernelGGL((k_net_z<S, 2048>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 4096)
+    hipLaunchKernelGGL((k_net_z<S, 4096>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else
-    hipLaunchKernelGGL((k_net_z<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+    hipLaunchKernelGGL((k_net_z<S, 0>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
 }
 
 void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,

@@ -90,10 +90,11 @@ __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* po
 // layer and its reduction.  Leaves fp [XB][64] (60 policy features + clock), red[bb*256] = value
 // pre-tanh.  xscale: the image holds x / xscale (a power of two; k_net_y's dynamic range).
 // F8LO (k_net_z's image): part 1 holds e4m3 bytes, the lo part of channel c at byte c of the
-// row's first 256 B (16-B chunks swizzled as ioff), in units of lo_scale (a power of two).
+// row's first 256 B (16-B chunks swizzled as ioff), board bb's in units of lo_scale[bb] (powers
+// of two).
 template <int NT = 256, bool F8LO = false>
 __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0, int nb, const NetWeights& W,
-                                             int tid, float xscale = 1.f, float lo_scale = 1.f) {
+                                             int tid, float xscale = 1.f, float4 lo_scale = {1.f, 1.f, 1.f, 1.f}) {
   float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
   float* fv = fp + XB * 64;                            // [XB][32]: vconv features (30) + clock
   float* red = fv + XB * 32;                           // [XB][256]
@@ -104,10 +105,11 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
     for (int c = 0; c < 32; ++c) {
       const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ioff(0, bb, p, c));
       if constexpr (F8LO) {
+        const float lsc = bb == 0 ? lo_scale.x : bb == 1 ? lo_scale.y : bb == 2 ? lo_scale.z : lo_scale.w;
         const uint2 q = *reinterpret_cast<const uint2*>(smem + ioff(1, bb, p, c >> 1) + 8 * (c & 1));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float lo = __builtin_amdgcn_cvt_f32_fp8((int)((j < 4 ? q.x : q.y) >> (8 * (j & 3))), 0) * lo_scale;
+          const float lo = __builtin_amdgcn_cvt_f32_fp8((int)((j < 4 ? q.x : q.y) >> (8 * (j & 3))), 0) * lsc;
           s += wr[8 * c + j] * ((float)xh[j] + lo);
         }
       } else {

@@ -93,8 +93,9 @@ class Engine:
 
     # ---- batched self-play -----------------------------------------------------------------------
     def set_precision(self, precision):
-        """'f16x3' (default: fp16 hi/lo split MFMA, fp32-accurate), 'f16f8' (the split's cross
-        terms on the block-scaled e4m3 MFMA, k_net_z: within 1e-5 of fp32) or 'fp32' (fp32 MFMA)."""
+        """'f16f8' (default, k_net_z: the fp16 split's cross terms on the block-scaled e4m3 MFMA,
+        within 2e-6 of fp32 on values), 'f16x3' (k_net_y: fp16 hi/lo split MFMA, within 1e-7) or
+        'fp32' (fp32 MFMA)."""
         _lib.check(self.L.mtaz_set_precision(self.h, {'fp32': 0, 'f16x3': 1, 'f16f8': 2}[precision]))
 
     def set_net_variant(self, variant):

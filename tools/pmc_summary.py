@@ -16,6 +16,9 @@ import re
 from collections import defaultdict
 
 
+KERNELS = set()
+
+
 def read_counters(root):
     """{counter: [per-dispatch value]} over every counter_collection CSV under root."""
     vals = defaultdict(dict)
@@ -24,6 +27,7 @@ def read_counters(root):
             for row in csv.DictReader(f):
                 if 'k_net_' not in row.get('Kernel_Name', ''):
                     continue
+                KERNELS.update(re.findall(r'k_net_[xyz]', row['Kernel_Name']))
                 key = (path, row['Dispatch_Id'])
                 name = row['Counter_Name']
                 vals[name][key] = vals[name].get(key, 0.0) + float(row['Counter_Value'])
@@ -52,14 +56,14 @@ def main():
     hit, miss = mean('TCC_HIT_sum'), mean('TCC_MISS_sum')
     games, sims, line = bench_config(args.root)
     out = {
-        'kernel': 'k_net_y',
+        'kernel': '+'.join(sorted(KERNELS)),
         'games': games, 'sims': sims,
         'dispatches': {k: len(v) for k, v in c.items()},
         'fetch_size_kb_per_launch': fetch_kb,
         'write_size_kb_per_launch': write_kb,
         'hbm_bytes_per_launch': (2 * fetch_kb + write_kb) * 1024 if fetch_kb is not None and write_kb is not None else None,
         'l2_hit_rate': hit / (hit + miss) if hit is not None and miss else None,
-        'method': 'rocprofv3 --pmc, one pass per counter group, --kernel-include-regex k_net_[xy]; '
+        'method': 'rocprofv3 --pmc, one pass per counter group, --kernel-include-regex k_net_[xyz]; '
                   'bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE half-count correction)',
     }
     if line is not None:
