@@ -108,6 +108,12 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   // their max, as k_net_y's
   auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next, const float* boundb) {
     constexpr bool conv_a = decltype(conv_a_t)::value;
+    // the lane's coordinates, opaque here: otherwise the compiler hoists the epilogue's 48 LDS
+    // addresses out of the layer loop and spills them, and every tile then waits on a scratch
+    // reload (about half of the epilogue's cycles)
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int n = el & 15, g = el >> 4, p1 = 16 + n;
     const float bound = fmaxf(fmaxf(boundb[0], boundb[1]), fmaxf(boundb[2], boundb[3]));
     const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
     const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
