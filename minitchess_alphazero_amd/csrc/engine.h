@@ -142,12 +142,26 @@ struct NetWeights {
   // part's power of two (127 - a).
   const uint4* conv8;
   const int32_t* conv8_sc;
+  // k_net_z VAR 8192 (cross terms in e2m3 = fp6): the same hi / lo parts as conv8, each block of
+  // 32 K (one output channel, tap, 32 input channels) in e2m3 with its own e8m0 scale:
+  // [L 18][cotile 16][group 36 = (tap, chunk, part)][112 x 16 B]; per group and lane l
+  // (co = 16*cotile + (l&15), channels 128*chunk + 32*(l>>4) + perm(q)): bytes 0..15 of the 24-B
+  // fp6 vector at 16 B x l, bytes 16..23 at 1024 + 8 l, the scale (u32, byte 0) at 1536 + 4 l.
+  // Value q of the vector (bits 6q..6q+5) is channel perm(q) = 16*((q>>2)&1) + 4*(q>>3) + (q&3)
+  // of the 32-channel block: the order in which the epilogue's lanes hold them.
+  const uint4* conv6;
+  // k_net_z VAR 262144 (ds_read_b64 operand reads): convy and conv8 with the two 8-byte halves of
+  // every 16 B swapped in the lanes of odd K group (l>>4): those lanes read their LDS fragments
+  // half-swapped, which keeps each 32-lane read group on distinct banks
+  const uint4* convz;
+  const uint4* conv8z;
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
 constexpr size_t CONVX_U4_PER_LAYER = (size_t)8 * 144 * 2 * 64;  // 147,456 x 16 B = 2.36 MB
 enum NetPrecision { NET_FP32 = 0, NET_F16X3 = 1, NET_F16F8 = 2 };
 constexpr size_t CONV8_U4_PER_LAYER = (size_t)16 * 9 * 2 * 2 * 2 * 64;   // 73,728 x 16 B = 1.18 MB
+constexpr size_t CONV6_U4_PER_LAYER = (size_t)16 * 36 * 112;   // 64,512 x 16 B = 1.03 MB
 constexpr int ERR_F16 = 512;   // activation exceeded the f16 range in the fp16x3 trunk
 
 struct NetBuffers {

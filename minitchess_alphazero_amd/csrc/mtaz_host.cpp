@@ -484,6 +484,13 @@ static uint8_t to_e4m3(double v) {
   return sgn | (uint8_t)(((e + 7) << 3) | (int)(m - 8));
 }
 
+// e2m3 (fp6: 1 sign, 2 exponent bits with bias 1, 3 mantissa bits) code of v, |v| <= 7.5, round
+// to nearest even: e4m3's grid below 2^-3 is e2m3's grid scaled by 2^-6, so round there
+static uint8_t to_e2m3(double v) {
+  const uint8_t b = to_e4m3(ldexp(v, -6));
+  return (uint8_t)((b & 0x1f) | ((b & 0x80) >> 2));
+}
+
 struct mtaz_engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -915,6 +922,47 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
                   dst[u4 * 16 + byte] = to_e4m3(ldexp(at(part, co, t * 256 + ci), a[part]));
                 }
   }
+  // k_net_z VAR 8192: the same parts in e2m3 blocks of 32 K with one e8m0 scale each
+  // (NetWeights::conv6)
+  std::vector<uint8_t> w6((size_t)CONV_LAYERS * CONV6_U4_PER_LAYER * 16, 0);
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const _Float16* src = wy.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    auto at = [&](int part, int co, int k) {
+      const int ct = co >> 4, kb = k >> 5, ln = (co & 15) + 16 * ((k & 31) >> 3);
+      return (double)src[((((size_t)ct * 72 + kb) * 2 + part) * 64 + ln) * 8 + (k & 7)];
+    };
+    uint8_t* dst = w6.data() + (size_t)L * CONV6_U4_PER_LAYER * 16;
+    for (int ct = 0; ct < 16; ++ct)
+      for (int t = 0; t < 9; ++t)
+        for (int c = 0; c < 2; ++c)
+          for (int part = 0; part < 2; ++part) {
+            uint8_t* gb = dst + ((((size_t)ct * 9 + t) * 2 + c) * 2 + part) * 112 * 16;
+            for (int lane = 0; lane < 64; ++lane) {
+              const int co = 16 * ct + (lane & 15);
+              double v[32], mx = 0;
+              for (int q = 0; q < 32; ++q) {
+                const int ci = 128 * c + 32 * (lane >> 4) + 16 * ((q >> 2) & 1) + 4 * (q >> 3) + (q & 3);
+                v[q] = at(part, co, t * 256 + ci);
+                mx = std::max(mx, fabs(v[q]));
+              }
+              int sc = -126;   // smallest s with mx * 2^-s <= 7.5
+              if (mx > 0) {
+                sc = ilogb(mx) - 2;
+                if (ldexp(mx, -sc) > 7.5) ++sc;
+                sc = std::max(-126, std::min(126, sc));
+              }
+              uint8_t bytes[24] = {0};
+              for (int q = 0; q < 32; ++q) {
+                const uint32_t code = to_e2m3(ldexp(v[q], -sc));
+                for (int b = 0; b < 6; ++b)
+                  if (code >> b & 1) bytes[(6 * q + b) >> 3] |= (uint8_t)(1u << ((6 * q + b) & 7));
+              }
+              memcpy(gb + 16 * lane, bytes, 16);
+              memcpy(gb + 1024 + 8 * lane, bytes + 16, 8);
+              gb[1536 + 4 * lane] = (uint8_t)(127 + sc);
+            }
+          }
+  }
   // k_net_y output bounds (NetWeights::yrange): per conv the max over output channels of the
   // L1 norm of the folded weights and the max |folded bias|; the stem's; max |embedding|.
   std::vector<float> yr(2 * CONV_LAYERS + 3);
@@ -946,8 +994,18 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   HIPCHK(hipMemcpy(h->wyrange, yr.data(), yr.size() * 4, hipMemcpyHostToDevice));
   h->w.yrange = h->wyrange;
   const size_t nx = wx.size() / 8, ns = sx.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
-  const size_t nsc = (sc8.size() + 3) / 4;
-  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, 2 * nx + ns + nsy + n8 + nsc));
+  const size_t nsc = (sc8.size() + 3) / 4, n6 = w6.size() / 16;
+  // half-swapped copies for the ds_read_b64 build (NetWeights::convz, conv8z)
+  std::vector<_Float16> wz(wy);
+  for (size_t u = 0; u < wz.size() / 8; ++u)
+    if (((u % 64) >> 4) & 1)
+      for (int j = 0; j < 4; ++j) std::swap(wz[u * 8 + j], wz[u * 8 + 4 + j]);
+  std::vector<uint8_t> w8z(w8);
+  for (size_t u = 0; u < w8z.size() / 16; ++u)
+    if (((u % 64) >> 4) & 1)
+      for (int j = 0; j < 8; ++j) std::swap(w8z[u * 16 + j], w8z[u * 16 + 8 + j]);
+  const size_t oz = 2 * nx + ns + nsy + n8 + nsc + n6;
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, oz + nx + n8));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
   HIPCHK(hipMemcpy(h->wxbuf, wx.data(), nx * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + nx, sx.data(), ns * 16, hipMemcpyHostToDevice));
@@ -955,6 +1013,9 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns, sy.data(), nsy * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy, w8.data(), n8 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy + n8, sc8.data(), sc8.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy + n8 + nsc, w6.data(), n6 * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + oz, wz.data(), nx * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + oz + nx, w8z.data(), n8 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx = h->wxbuf;
   h->w.convx_inv = h->wxinv;
@@ -964,6 +1025,9 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.stemy = h->wxbuf + 2 * nx + ns;
   h->w.conv8 = h->wxbuf + 2 * nx + ns + nsy;
   h->w.conv8_sc = reinterpret_cast<const int32_t*>(h->wxbuf + 2 * nx + ns + nsy + n8);
+  h->w.conv6 = h->wxbuf + 2 * nx + ns + nsy + n8 + nsc;
+  h->w.convz = h->wxbuf + oz;
+  h->w.conv8z = h->wxbuf + oz + nx;
   h->weights_ok = true;
   return 0;
 }

@@ -43,6 +43,13 @@ __device__ __forceinline__ i32x8 cat8(uint4 a, uint4 b) {
   return (i32x8){(int)a.x, (int)a.y, (int)a.z, (int)a.w, (int)b.x, (int)b.y, (int)b.z, (int)b.w};
 }
 
+// 16 B at p as two 8-B reads, the half at byte h (0 or 8) first
+__device__ __forceinline__ uint4 rd8x2(const char* p, int h) {
+  const uint2 a = *reinterpret_cast<const uint2*>(p + h), b = *reinterpret_cast<const uint2*>(p + (h ^ 8));
+  return make_uint4(a.x, a.y, b.x, b.y);
+}
+__device__ __forceinline__ f16x8 rd16x2(const char* p, int h) { return __builtin_bit_cast(f16x8, rd8x2(p, h)); }
+
 // 4 e4m3 bytes of {a, b, c, d} (round to nearest even, OCP e4m3fn)
 __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d) {
   int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
@@ -60,6 +67,20 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
                                                                float* __restrict__ values_out,
                                                                unsigned long long* __restrict__ stamps) {
   constexpr int NW = zWaves<VAR>, NT = 64 * NW, CT = 16 / NW;   // waves, threads, channel tiles per wave
+  constexpr bool F6 = (VAR & 8192) != 0;   // cross terms in e2m3 blocks (epilogue6, NetWeights::conv6)
+  // diagnostic builds (timing only, wrong results): 16384 = every layer reads layer 0's weights
+  // (an L2-resident weight set), 32768 = every step reads k-block / group 0 (L1-resident)
+  constexpr bool DIAG_L2 = (VAR & 16384) != 0, DIAG_L1 = (VAR & 32768) != 0;
+  // 65536 = no cross-term MFMAs (phase B issues its loads only), 131072 = no activation LDS reads
+  // in the K loop (the fragments of step 0 are reused)
+  constexpr bool DIAG_NOB = (VAR & 65536) != 0, DIAG_NOLDS = (VAR & 131072) != 0;
+  // 262144: activation fragments by ds_read_b64 pairs, the lanes of odd K group reading each 16 B
+  // upper half first (weights: NetWeights::convz / conv8z; e2m3 blocks: stored half-swapped by the
+  // odd waves), so that the 32 lanes of a read group cover every bank once (4.9 LDS cycles per
+  // 16 B on the K loop's access pattern vs 7.2 for ds_read_b128, tools/lds_conflicts.py)
+  constexpr bool R64 = (VAR & 262144) != 0;
+  constexpr bool TBL = (VAR & 524288) != 0;   // per-row swizzle table (net_common.h hz)
+  static_assert(!F6 || NW == 8, "the e2m3 epilogue assumes 8 waves of 32 channels");
   __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
@@ -144,9 +165,9 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         f32x4v& a = acc[ct * 8 + t];
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
-          const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1);
-          const int al8 = ioff(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
-          const int ah8 = ioff(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
+          const int ah = ioffs<TBL>(0, bb, p, co0 >> 3) + 8 * (g & 1);
+          const int al8 = ioffs<TBL>(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
+          const int ah8 = ioffs<TBL>(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
           float y[4];
           y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
           y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
@@ -204,6 +225,154 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     slot ^= 1;
   };
 
+  // VAR 8192 epilogue: the cross-term copies in e2m3 (fp6) blocks instead of e4m3 bytes.  Wave w
+  // owns the 32 output channels of block w (= K block 4c + g of the next conv's 128-channel chunk
+  // c), and per square its lane g holds channels 16 ct + 4 g + i (ct, i < 4): values 8 g + 4 ct + i
+  // of the block's 32-value fp6 vector (NetWeights::conv6 packs the weights in that order), bits
+  // 48 g .. 48 g + 47 = bytes 6 g .. 6 g + 5 of the 32-B block slot (term 0: Xl, chunks 2 w, 2 w + 1
+  // of part 1; term 1: Xh, chunks 16 + 2 w, 17 + 2 w), its e8m0 scale at byte 24.  The scale
+  // covers the block's largest |value| (a rounded-up 16-bit key, max over the 4 lanes g), so that
+  // every value is <= 7.5 in scaled units; codes by e4m3 RNE of v * 2^(-s-6) (fp6_scale_probe).
+  auto epilogue6 = [&](float inv, const float* bias, auto conv_a_t, float s_next, const float* boundb) {
+    constexpr bool conv_a = decltype(conv_a_t)::value;
+    int el = lane;
+    asm volatile("" : "+v"(el));
+    const int n = el & 15, g = el >> 4, p1 = 16 + n;
+    const float bound = fmaxf(fmaxf(boundb[0], boundb[1]), fmaxf(boundb[2], boundb[3]));
+    const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
+    const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
+    const float sseed = __builtin_ldexpf(s_next, xs - xo);
+    const int bx = R64 ? 8 * (wave & 1) : 0;   // half-swapped block slots (odd waves, R64)
+    const int o32 = ((g & 1) ? 6 * g + 2 : 6 * g) ^ bx, o16 = ((g & 1) ? 6 * g : 6 * g + 4) ^ bx, osc = 24 ^ bx;
+    float4 bv[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const float4 bu = *reinterpret_cast<const float4*>(bias + 32 * wave + 16 * ct + 4 * g);
+      bv[ct] = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
+    }
+    // byte address of byte `b` of this wave's block slot of term `term` on row p of board bb
+    auto baddr = [&](int term, int bb, int p, int b) {
+      return ioffs<TBL>(1, bb, p, 16 * term + 2 * wave + (b >> 4)) + (b & 15);
+    };
+    float ymax[XB] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int bb = t >> 1, pt = t & 1;
+      const bool valid = pt == 0 || p1 < 30;
+      const int p = pt ? (valid ? p1 : ZROW) : n;
+      float y[8];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const f32x4v& a = acc[ct * 8 + t];
+        y[4 * ct + 0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv[ct].x), 0.f);
+        y[4 * ct + 1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv[ct].y), 0.f);
+        y[4 * ct + 2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv[ct].z), 0.f);
+        y[4 * ct + 3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv[ct].w), 0.f);
+      }
+      if (!valid) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ymax[bb] = fmaxf(ymax[bb], y[k]);
+      if constexpr (conv_a) {
+        // seed conv B with the block input Xh + Xl (conv B's units)
+        float xin[8];
+        if (valid) {
+          const uint32_t r32 = *reinterpret_cast<const uint32_t*>(smem + baddr(0, bb, p, o32));
+          const uint32_t r16 = *reinterpret_cast<const uint16_t*>(smem + baddr(0, bb, p, o16));
+          const int sb = *reinterpret_cast<const uint8_t*>(smem + baddr(0, bb, p, osc));
+          const uint32_t P0 = (g & 1) ? (r16 | (r32 << 16)) : r32, P1 = (g & 1) ? (r32 >> 16) : r16;
+          const uint32_t A24 = P0 & 0xffffffu, B24 = (P0 >> 24) | (P1 << 8);
+          const float lsc = __builtin_ldexpf(sseed, sb - 127 + 6);
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) {
+            const uint32_t c = ct ? B24 : A24;
+            uint32_t e = (c & 0x3fu) | ((c << 2) & 0x3f00u) | ((c << 4) & 0x3f0000u) | ((c << 6) & 0x3f000000u);
+            e = (e & 0x1f1f1f1fu) | ((e & 0x20202020u) << 2);
+            const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * wave + 2 * ct + (g >> 1)) + 8 * (g & 1));
+            xin[4 * ct + 0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 0) * lsc);
+            xin[4 * ct + 1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 1) * lsc);
+            xin[4 * ct + 2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 2) * lsc);
+            xin[4 * ct + 3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 3) * lsc);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) xin[k] = 0.f;
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct * 8 + t] = (f32x4v){xin[4 * ct], xin[4 * ct + 1], xin[4 * ct + 2], xin[4 * ct + 3]};
+      } else {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct * 8 + t] = (f32x4v){0};
+      }
+      // hi / lo split, block keys: bf16 bits rounded up (>= the value) of max h, max |l|
+      float h[8], l[8], mh = 0.f, ml = 0.f;
+      f16x4 yh[2];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const _Float16 hh = (_Float16)y[k];
+        yh[k >> 2][k & 3] = hh;
+        h[k] = (float)hh;
+        l[k] = y[k] - h[k];
+        mh = fmaxf(mh, h[k]);
+        ml = fmaxf(ml, fabsf(l[k]));
+      }
+      uint32_t key = (((__float_as_uint(mh) + 0xffffu) >> 16) << 16) | ((__float_as_uint(ml) + 0xffffu) >> 16);
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const uint32_t other = (uint32_t)__shfl_xor((int)key, o, 64);
+        key = (max(key >> 16, other >> 16) << 16) | max(key & 0xffffu, other & 0xffffu);
+      }
+      if (valid) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+          *reinterpret_cast<f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * wave + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
+      }
+#pragma unroll
+      for (int term = 0; term < 2; ++term) {
+        const uint32_t K = term ? key >> 16 : key & 0xffffu;
+        int s = (int)((K >> 7) & 0xffu) - 129 + ((K & 0x7fu) > 112u ? 1 : 0);
+        s = s < -120 ? -120 : s > 120 ? 120 : s;
+        const float f = __builtin_ldexpf(1.f, -s - 6);
+        const float* v = term ? h : l;
+        uint32_t c24[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          uint32_t d = pk_fp8x4(v[4 * ct] * f, v[4 * ct + 1] * f, v[4 * ct + 2] * f, v[4 * ct + 3] * f);
+          d = (d & 0x1f1f1f1fu) | ((d >> 2) & 0x20202020u);
+          c24[ct] = (d & 0x3fu) | ((d >> 2) & 0xfc0u) | ((d >> 4) & 0x3f000u) | ((d >> 6) & 0xfc0000u);
+        }
+        const uint32_t P0 = c24[0] | (c24[1] << 24), P1 = c24[1] >> 8;
+        const uint32_t w32 = (g & 1) ? ((P0 >> 16) | (P1 << 16)) : P0;
+        const uint32_t w16 = (g & 1) ? (P0 & 0xffffu) : P1;
+        if (valid) {
+          *reinterpret_cast<uint32_t*>(smem + baddr(term, bb, p, o32)) = w32;
+          *reinterpret_cast<uint16_t*>(smem + baddr(term, bb, p, o16)) = (uint16_t)w16;
+          if (g == 0) *reinterpret_cast<uint8_t*>(smem + baddr(term, bb, p, osc)) = (uint8_t)(127 + s);
+        }
+      }
+    }
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) ymax[bb] = fmaxf(ymax[bb], __shfl_xor(ymax[bb], o, 64));
+    }
+    if (lane < XB) {
+      const float m = lane == 0 ? ymax[0] : lane == 1 ? ymax[1] : lane == 2 ? ymax[2] : ymax[3];
+      atomicMax(&mxs[slot * XB + lane], __float_as_uint(m));
+    }
+    if (tid < XB) mxs[(slot ^ 1) * XB + tid] = 0u;
+    xs = xo;
+    __syncthreads();
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) {
+      mxb[bb] = __builtin_ldexpf(__uint_as_float(mxs[slot * XB + bb]), xo);
+      if (!__builtin_isfinite(mxb[bb])) overflow = 1;
+    }
+    slot ^= 1;
+  };
+
   // ---------------- stem: conv3x3 8->256 in f16x3 (k_net_y's), K = 3 k-blocks -------------
   // (stem_input zeroes both parts' zero rows, which covers [Xl8 | Xh8] of the zero row)
   char* simg = smem + IMGB;
@@ -244,7 +413,10 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #pragma unroll
     for (int bb = 0; bb < XB; ++bb)
       bnd[bb] = __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mxb[bb], W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f;
-    epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f, bnd);
+    if constexpr (F6)
+      epilogue6(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f, bnd);
+    else
+      epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f, bnd);
   }
   stamp(st_stem);
 
@@ -256,24 +428,35 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   f16x8 A16[RA][CT], B16[8];
   i32x8 A8[RG][CT], B8[4];
   const int n_ = n, p1_ = p1, ph0_ = ph0, pw0_ = pw0, ph1_ = ph1, pw1_ = pw1, g_ = g;
-  const uint4* Wh = W.convy + (size_t)(CT * wave) * KBZ * 128 + lane;          // hi parts of convy
-  const uint4* W8 = W.conv8 + (size_t)(CT * wave) * GZ * 128 + lane;
+  const uint4* Wh = (R64 ? W.convz : W.convy) + (size_t)(CT * wave) * KBZ * 128 + lane;   // hi parts
+  const uint4* W8 = (R64 ? W.conv8z : W.conv8) + (size_t)(CT * wave) * GZ * 128 + lane;
+  const uint4* W6 = W.conv6 + (size_t)(CT * wave) * GZ * 112;
   const int32_t* sc8 = W.conv8_sc;
 
   // Wh fragments of step (k-block) KB, the wave's channel tiles
 #define Z_LOAD_A16(S, KB)                                                             \
   {                                                                                   \
-    const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
+    const int kk_ = DIAG_L1 ? 0 : (KB) < KBZ ? (KB) : KBZ - 1;                        \
     _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_)                                 \
       S[c_] = __builtin_bit_cast(f16x8, Wh[((size_t)c_ * KBZ + kk_) * 128]);          \
   }
-  // e4m3 weight fragments of group GR (tap, chunk, term), channel tiles [C0, C0 + CT/2)
+  // e4m3 weight fragments of group GR (tap, chunk, term), channel tiles [C0, C0 + CT/2); with
+  // F6 the e2m3 vector in dwords 0..5 and the lane's e8m0 scale in dword 6
 #define Z_LOAD_A8(S, GR, C0)                                                          \
   {                                                                                   \
-    const int gg_ = (GR) < GZ ? (GR) : GZ - 1;                                        \
+    const int gg_ = DIAG_L1 ? 0 : (GR) < GZ ? (GR) : GZ - 1;                          \
     _Pragma("unroll") for (int c_ = (C0); c_ < (C0) + CT / 2; ++c_) {                 \
-      const uint4* p_ = W8 + ((size_t)c_ * GZ + gg_) * 128;                           \
-      S[c_] = cat8(p_[0], p_[64]);                                                    \
+      if constexpr (F6) {                                                             \
+        const uint4* p_ = W6 + ((size_t)c_ * GZ + gg_) * 112;                         \
+        const uint4 d0_ = p_[lane];                                                   \
+        const uint2 d1_ = reinterpret_cast<const uint2*>(p_ + 64)[lane];              \
+        const uint32_t sc_ = reinterpret_cast<const uint32_t*>(p_ + 96)[lane];        \
+        S[c_] = (i32x8){(int)d0_.x, (int)d0_.y, (int)d0_.z, (int)d0_.w,               \
+                        (int)d1_.x, (int)d1_.y, (int)sc_, 0};                         \
+      } else {                                                                        \
+        const uint4* p_ = W8 + ((size_t)c_ * GZ + gg_) * 128;                         \
+        S[c_] = cat8(p_[0], p_[64]);                                                  \
+      }                                                                               \
     }                                                                                 \
   }
   // Xh (f16) fragments of step KB for both square tiles: S16[2 * board + tile]
@@ -282,12 +465,18 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
     const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
     const int r0_ = src_row(n, ph0, pw0, tap_), r1_ = src_row(p1, ph1, pw1, tap_);    \
-    const int o0_ = r0_ * RB + ((ch_ ^ (r0_ & 15)) << 4);                             \
-    const int o1_ = r1_ * RB + ((ch_ ^ (r1_ & 15)) << 4);                             \
+    const int o0_ = r0_ * RB + ((ch_ ^ swz<TBL>(r0_)) << 4);                          \
+    const int o1_ = r1_ * RB + ((ch_ ^ swz<TBL>(r1_)) << 4);                          \
     _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
       const char* base_ = smem + bb_ * IROWS * RB;                                    \
-      S16[2 * bb_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                   \
-      S16[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);               \
+      if constexpr (R64) {                                                            \
+        const int h_ = 8 * (g & 1);                                                   \
+        S16[2 * bb_] = rd16x2(smem + bofs[bb_] + o0_, h_);                            \
+        S16[2 * bb_ + 1] = rd16x2(smem + bofs[bb_] + o1_, h_);                        \
+      } else {                                                                        \
+        S16[2 * bb_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                 \
+        S16[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);             \
+      }                                                                               \
     }                                                                                 \
   }
   // e4m3 fragments of step KB's group on square tile KB & 1 (Xl8 for term 0, Xh8 for term 1):
@@ -299,11 +488,17 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     const int r_ = (kk_ & 1) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_); \
     const int q0_ = 16 * term_ + 8 * cc_ + 2 * g;                                     \
     /* part-1 row base once, so that the boards' offsets (< 64 KB) fit the ds_read immediate */ \
-    const char* p0_ = smem + PARTB + r_ * RB + ((q0_ ^ (r_ & 15)) << 4);              \
-    const char* p1_ = smem + PARTB + r_ * RB + (((q0_ + 1) ^ (r_ & 15)) << 4);        \
-    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                              \
-      S8[bb_] = cat8(*reinterpret_cast<const uint4*>(p0_ + bb_ * IROWS * RB),        \
-                     *reinterpret_cast<const uint4*>(p1_ + bb_ * IROWS * RB));       \
+    const char* p0_ = smem + PARTB + r_ * RB + ((q0_ ^ swz<TBL>(r_)) << 4);           \
+    const char* p1_ = smem + PARTB + r_ * RB + (((q0_ + 1) ^ swz<TBL>(r_)) << 4);     \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
+      if constexpr (R64) {                                                            \
+        const int h_ = 8 * (g & 1);                                                   \
+        S8[bb_] = cat8(rd8x2(p0_ + bofs[bb_], h_), rd8x2(p1_ + bofs[bb_], h_));       \
+      } else {                                                                        \
+        S8[bb_] = cat8(*reinterpret_cast<const uint4*>(p0_ + bb_ * IROWS * RB),      \
+                       *reinterpret_cast<const uint4*>(p1_ + bb_ * IROWS * RB));     \
+      }                                                                               \
+    }                                                                                 \
   }
 
   for (int L = 0; L < CONV_LAYERS; ++L) {
@@ -312,6 +507,10 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     // layer loop into ~150 VGPRs
     int n = n_, p1 = p1_, ph0 = ph0_, pw0 = pw0_, ph1 = ph1_, pw1 = pw1_, g = g_;
     asm volatile("" : "+v"(n), "+v"(p1), "+v"(ph0), "+v"(pw0), "+v"(ph1), "+v"(pw1), "+v"(g));
+    // R64: board offsets opaque, so that the compiler does not pair two boards' 8-B reads into
+    // one ds_read2st64_b64 (16-lane bank groups: half ds_read_b64's rate)
+    int bofs[XB] = {0, IROWS * RB, 2 * IROWS * RB, 3 * IROWS * RB};
+    if constexpr (R64) asm volatile("" : "+s"(bofs[0]), "+s"(bofs[1]), "+s"(bofs[2]), "+s"(bofs[3]));
     const int sa_h = sc8[2 * L], sa_l = sc8[2 * L + 1];
     int sb_l[XB], sb_h[XB];   // the input image's e4m3 units, per board
 #pragma unroll
@@ -324,6 +523,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
       Z_LOAD_A8(A8[p], p, CT / 2)
     }
     Z_LOAD_B16(B16, 0);
+    if constexpr (DIAG_NOLDS) Z_LOAD_B8(B8, 0);
 #pragma unroll 1
     for (int s0 = 0; s0 < KBZ; s0 += U) {
 #pragma unroll
@@ -332,7 +532,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         // phase A: Wh x Xh of k-block s on every column tile; meanwhile this step's e4m3
         // activation fragments and the Wh fragments PD steps ahead
         __builtin_amdgcn_sched_barrier(0);
-        Z_LOAD_B8(B8, s);
+        if constexpr (!DIAG_NOLDS) Z_LOAD_B8(B8, s);
         Z_LOAD_A16(A16[(u + PD) % RA], s + PD);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
@@ -342,7 +542,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         // phase B: group s/2 on square tile s&1; meanwhile the next step's Xh fragments and half
         // of the e4m3 weight group GD groups ahead
         __builtin_amdgcn_sched_barrier(0);
-        Z_LOAD_B16(B16, s + 1);
+        if constexpr (!DIAG_NOLDS) Z_LOAD_B16(B16, s + 1);
         Z_LOAD_A8(A8[((u >> 1) + GD) % RG], (s >> 1) + GD, (CT / 2) * (u & 1));
         const int pt = u & 1;
         const bool term = (u >> 1) & 1;
@@ -350,14 +550,25 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-          for (int bb = 0; bb < XB; ++bb)
-            acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 0, 0, 0, sa, 0,
-                term ? sb_h[bb] : sb_l[bb]);
+          for (int bb = 0; bb < XB; ++bb) {
+            if constexpr (DIAG_NOB)
+              ;
+            else if constexpr (F6)
+              acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                  A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 2, 2, 0, A8[(u >> 1) % RG][ct][6], 0,
+                  B8[bb][6]);
+            else
+              acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                  A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 0, 0, 0, sa, 0,
+                  term ? sb_h[bb] : sb_l[bb]);
+          }
       }
     }
-    Wh += CONVX_U4_PER_LAYER;
-    W8 += CONV8_U4_PER_LAYER;
+    if constexpr (!DIAG_L2 && !DIAG_L1) {
+      Wh += CONVX_U4_PER_LAYER;
+      W8 += CONV8_U4_PER_LAYER;
+      W6 += CONV6_U4_PER_LAYER;
+    }
     __syncthreads();
     stamp(st_k);   // (k_net_z: the K-loop share includes the wait for the workgroup's slowest wave)
     float bnd[XB];
@@ -367,12 +578,19 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         bnd[bb] = __builtin_fmaf(W.yrange[2 * L], mxb[bb], W.yrange[2 * L + 1]) * 1.0009765625f;
         mxblk[bb] = mxb[bb];
       }
-      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bnd);
+      if constexpr (F6)
+        epilogue6(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bnd);
+      else
+        epilogue(W.convx_inv[L], W.conv_b + L * 256, std::true_type{}, 1.0f / W.convx_inv[L + 1], bnd);
     } else {
 #pragma unroll
       for (int bb = 0; bb < XB; ++bb)
         bnd[bb] = (__builtin_fmaf(W.yrange[2 * L], mxb[bb], W.yrange[2 * L + 1]) + mxblk[bb]) * 1.0009765625f;
-      epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bnd);
+      // (F6: the last conv stores e4m3 bytes, the image heads_reduce reads)
+      if (F6 && L < CONV_LAYERS - 1)
+        epilogue6(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bnd);
+      else
+        epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bnd);
     }
     stamp(st_epi);
   }
@@ -380,9 +598,9 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #undef Z_LOAD_A8
 #undef Z_LOAD_B16
 #undef Z_LOAD_B8
-  if (overflow) atomicOr(D.pr.err, ERR_F16);
+  if (overflow && !DIAG_L2 && !DIAG_L1 && !DIAG_NOB && !DIAG_NOLDS) atomicOr(D.pr.err, ERR_F16);
 
-  heads_reduce<NT, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
+  heads_reduce<NT, true, TBL>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
                          make_float4(__builtin_ldexpf(1.f, -(sh[0] + 11)), __builtin_ldexpf(1.f, -(sh[1] + 11)),
                                      __builtin_ldexpf(1.f, -(sh[2] + 11)), __builtin_ldexpf(1.f, -(sh[3] + 11))));
   stamp(st_heads);
@@ -403,7 +621,29 @@ template <bool S>
 static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
-  if (var & 2048)
+  if (var == 524288)
+    hipLaunchKernelGGL((k_net_z<S, 524288>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 524288 + 8192)
+    hipLaunchKernelGGL((k_net_z<S, 524288 + 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 262144)
+    hipLaunchKernelGGL((k_net_z<S, 262144>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 262144 + 8192)
+    hipLaunchKernelGGL((k_net_z<S, 262144 + 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 16384)
+    hipLaunchKernelGGL((k_net_z<S, 16384>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 65536)
+    hipLaunchKernelGGL((k_net_z<S, 65536>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 131072)
+    hipLaunchKernelGGL((k_net_z<S, 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 65536 + 131072)
+    hipLaunchKernelGGL((k_net_z<S, 65536 + 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 8192 + 131072)
+    hipLaunchKernelGGL((k_net_z<S, 8192 + 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 32768)
+    hipLaunchKernelGGL((k_net_z<S, 32768>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 8192)
+    hipLaunchKernelGGL((k_net_z<S, 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var & 2048)
     hipLaunchKernelGGL((k_net_z<S, 2048>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 4096)
     hipLaunchKernelGGL((k_net_z<S, 4096>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);

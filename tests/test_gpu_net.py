@@ -28,7 +28,9 @@ def _softmax(x):
 NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4), 'f16x3-y128': ('f16x3', 128),
                'f16x3-y8': ('f16x3', 8), 'f16x3-x': ('f16x3', 512), 'f16x3-y2048': ('f16x3', 2048),
                'f16x3-y6144': ('f16x3', 6144), 'f16f8': ('f16f8', 0), 'f16f8-w4': ('f16f8', 2048),
-               'f16f8-deep': ('f16f8', 4096)}
+               'f16f8-deep': ('f16f8', 4096), 'f16f6': ('f16f8', 8192),
+               'f16f8-r64': ('f16f8', 262144), 'f16f6-r64': ('f16f8', 270336),
+               'f16f8-tbl': ('f16f8', 524288), 'f16f6-tbl': ('f16f8', 532480)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
@@ -148,8 +150,8 @@ def _wide_range_net(gain=6.0):
     return net.eval()
 
 
-@pytest.mark.parametrize('precision', ['f16x3', 'f16f8'])
-def test_dynamic_range_beyond_f16(precision):
+@pytest.mark.parametrize('precision,var', [('f16x3', 0), ('f16f8', 0), ('f16f8', 8192)])
+def test_dynamic_range_beyond_f16(precision, var):
     """k_net_y and k_net_z keep fp32's range (a per-workgroup power-of-two image scale chosen from a weight
     bound).  With trunk activations ~7e6 the logits match torch's fp32 eval forward to 1e-5 of
     each row's largest logit (the fp32 error scale at these magnitudes), values (saturated tanh)
@@ -163,6 +165,7 @@ def test_dynamic_range_beyond_f16(precision):
     fens = random_fens(129, seed=9)
     eng = Engine(n_games=64, sims=4)
     eng.set_precision(precision)
+    eng.set_net_variant(var)
     eng.set_weights(net)
     pos = np.stack([pos_from_fen(f) for f in fens])
     logits, values = eng.evaluate(pos)
