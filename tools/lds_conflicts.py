@@ -18,7 +18,7 @@ for off-board taps), chunk 4 (kk & 7) + g (f16 fragments) or the chunk pair
 
 Measured (bench_net, profiles/r01_z2/): the table cut the model's cycles per read from 7.2 to
 5.3 and SQ_LDS_BANK_CONFLICT accordingly, but not the K loop's time (+2% e4m3, -4% e2m3), and
-the ds_read_b64 form (VAR 262144, 4.9 cycles per 16 B in the model) took 21% longer: the K loop
+the ds_read_b64 form (VAR 262144, 4.9 cycles per 16 B in the model) took 23% longer: the K loop
 is not bound by LDS bank cycles.
 """
 import argparse
