@@ -80,7 +80,6 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   // 16 B on the K loop's access pattern vs 7.2 for ds_read_b128, tools/lds_conflicts.py)
   constexpr bool R64 = (VAR & 262144) != 0;
   constexpr bool TBL = (VAR & 524288) != 0;   // per-row swizzle table (net_common.h hz)
-  static_assert(!F6 || NW == 8, "the e2m3 epilogue assumes 8 waves of 32 channels");
   __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
@@ -242,114 +241,119 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
     const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
     const float sseed = __builtin_ldexpf(s_next, xs - xo);
-    const int bx = R64 ? 8 * (wave & 1) : 0;   // half-swapped block slots (odd waves, R64)
-    const int o32 = ((g & 1) ? 6 * g + 2 : 6 * g) ^ bx, o16 = ((g & 1) ? 6 * g : 6 * g + 4) ^ bx, osc = 24 ^ bx;
-    float4 bv[2];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const float4 bu = *reinterpret_cast<const float4*>(bias + 32 * wave + 16 * ct + 4 * g);
-      bv[ct] = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
-    }
-    // byte address of byte `b` of this wave's block slot of term `term` on row p of board bb
-    auto baddr = [&](int term, int bb, int p, int b) {
-      return ioffs<TBL>(1, bb, p, 16 * term + 2 * wave + (b >> 4)) + (b & 15);
-    };
     float ymax[XB] = {0.f, 0.f, 0.f, 0.f};
+    // wave w owns blocks (CT/2) w .. (CT/2) w + CT/2 - 1 (one with 8 waves, two with 4)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int bb = t >> 1, pt = t & 1;
-      const bool valid = pt == 0 || p1 < 30;
-      const int p = pt ? (valid ? p1 : ZROW) : n;
-      float y[8];
-#pragma unroll
+    for (int bi = 0; bi < CT / 2; ++bi) {
+      const int blk = (CT / 2) * wave + bi;
+      const int bx = R64 ? 8 * (blk & 1) : 0;   // half-swapped block slots (odd blocks, R64)
+      const int o32 = ((g & 1) ? 6 * g + 2 : 6 * g) ^ bx, o16 = ((g & 1) ? 6 * g : 6 * g + 4) ^ bx, osc = 24 ^ bx;
+      float4 bv[2];
+  #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        const f32x4v& a = acc[ct * 8 + t];
-        y[4 * ct + 0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv[ct].x), 0.f);
-        y[4 * ct + 1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv[ct].y), 0.f);
-        y[4 * ct + 2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv[ct].z), 0.f);
-        y[4 * ct + 3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv[ct].w), 0.f);
+        const float4 bu = *reinterpret_cast<const float4*>(bias + 32 * blk + 16 * ct + 4 * g);
+        bv[ct] = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
       }
-      if (!valid) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) y[k] = 0.f;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ymax[bb] = fmaxf(ymax[bb], y[k]);
-      if constexpr (conv_a) {
-        // seed conv B with the block input Xh + Xl (conv B's units)
-        float xin[8];
-        if (valid) {
-          const uint32_t r32 = *reinterpret_cast<const uint32_t*>(smem + baddr(0, bb, p, o32));
-          const uint32_t r16 = *reinterpret_cast<const uint16_t*>(smem + baddr(0, bb, p, o16));
-          const int sb = *reinterpret_cast<const uint8_t*>(smem + baddr(0, bb, p, osc));
-          const uint32_t P0 = (g & 1) ? (r16 | (r32 << 16)) : r32, P1 = (g & 1) ? (r32 >> 16) : r16;
-          const uint32_t A24 = P0 & 0xffffffu, B24 = (P0 >> 24) | (P1 << 8);
-          const float lsc = __builtin_ldexpf(sseed, sb - 127 + 6);
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) {
-            const uint32_t c = ct ? B24 : A24;
-            uint32_t e = (c & 0x3fu) | ((c << 2) & 0x3f00u) | ((c << 4) & 0x3f0000u) | ((c << 6) & 0x3f000000u);
-            e = (e & 0x1f1f1f1fu) | ((e & 0x20202020u) << 2);
-            const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * wave + 2 * ct + (g >> 1)) + 8 * (g & 1));
-            xin[4 * ct + 0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 0) * lsc);
-            xin[4 * ct + 1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 1) * lsc);
-            xin[4 * ct + 2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 2) * lsc);
-            xin[4 * ct + 3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 3) * lsc);
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) xin[k] = 0.f;
-        }
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[ct * 8 + t] = (f32x4v){xin[4 * ct], xin[4 * ct + 1], xin[4 * ct + 2], xin[4 * ct + 3]};
-      } else {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[ct * 8 + t] = (f32x4v){0};
-      }
-      // hi / lo split, block keys: bf16 bits rounded up (>= the value) of max h, max |l|
-      float h[8], l[8], mh = 0.f, ml = 0.f;
-      f16x4 yh[2];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const _Float16 hh = (_Float16)y[k];
-        yh[k >> 2][k & 3] = hh;
-        h[k] = (float)hh;
-        l[k] = y[k] - h[k];
-        mh = fmaxf(mh, h[k]);
-        ml = fmaxf(ml, fabsf(l[k]));
-      }
-      uint32_t key = (((__float_as_uint(mh) + 0xffffu) >> 16) << 16) | ((__float_as_uint(ml) + 0xffffu) >> 16);
-#pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-        const uint32_t other = (uint32_t)__shfl_xor((int)key, o, 64);
-        key = (max(key >> 16, other >> 16) << 16) | max(key & 0xffffu, other & 0xffffu);
-      }
-      if (valid) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-          *reinterpret_cast<f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * wave + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
-      }
-#pragma unroll
-      for (int term = 0; term < 2; ++term) {
-        const uint32_t K = term ? key >> 16 : key & 0xffffu;
-        int s = (int)((K >> 7) & 0xffu) - 129 + ((K & 0x7fu) > 112u ? 1 : 0);
-        s = s < -120 ? -120 : s > 120 ? 120 : s;
-        const float f = __builtin_ldexpf(1.f, -s - 6);
-        const float* v = term ? h : l;
-        uint32_t c24[2];
-#pragma unroll
+      // byte address of byte `b` of block blk's slot of term `term` on row p of board bb
+      auto baddr = [&](int term, int bb, int p, int b) {
+        return ioffs<TBL>(1, bb, p, 16 * term + 2 * blk + (b >> 4)) + (b & 15);
+      };
+  #pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int bb = t >> 1, pt = t & 1;
+        const bool valid = pt == 0 || p1 < 30;
+        const int p = pt ? (valid ? p1 : ZROW) : n;
+        float y[8];
+  #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
-          uint32_t d = pk_fp8x4(v[4 * ct] * f, v[4 * ct + 1] * f, v[4 * ct + 2] * f, v[4 * ct + 3] * f);
-          d = (d & 0x1f1f1f1fu) | ((d >> 2) & 0x20202020u);
-          c24[ct] = (d & 0x3fu) | ((d >> 2) & 0xfc0u) | ((d >> 4) & 0x3f000u) | ((d >> 6) & 0xfc0000u);
+          const f32x4v& a = acc[(2 * bi + ct) * 8 + t];
+          y[4 * ct + 0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv[ct].x), 0.f);
+          y[4 * ct + 1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv[ct].y), 0.f);
+          y[4 * ct + 2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv[ct].z), 0.f);
+          y[4 * ct + 3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv[ct].w), 0.f);
         }
-        const uint32_t P0 = c24[0] | (c24[1] << 24), P1 = c24[1] >> 8;
-        const uint32_t w32 = (g & 1) ? ((P0 >> 16) | (P1 << 16)) : P0;
-        const uint32_t w16 = (g & 1) ? (P0 & 0xffffu) : P1;
+        if (!valid) {
+  #pragma unroll
+          for (int k = 0; k < 8; ++k) y[k] = 0.f;
+        }
+  #pragma unroll
+        for (int k = 0; k < 8; ++k) ymax[bb] = fmaxf(ymax[bb], y[k]);
+        if constexpr (conv_a) {
+          // seed conv B with the block input Xh + Xl (conv B's units)
+          float xin[8];
+          if (valid) {
+            const uint32_t r32 = *reinterpret_cast<const uint32_t*>(smem + baddr(0, bb, p, o32));
+            const uint32_t r16 = *reinterpret_cast<const uint16_t*>(smem + baddr(0, bb, p, o16));
+            const int sb = *reinterpret_cast<const uint8_t*>(smem + baddr(0, bb, p, osc));
+            const uint32_t P0 = (g & 1) ? (r16 | (r32 << 16)) : r32, P1 = (g & 1) ? (r32 >> 16) : r16;
+            const uint32_t A24 = P0 & 0xffffffu, B24 = (P0 >> 24) | (P1 << 8);
+            const float lsc = __builtin_ldexpf(sseed, sb - 127 + 6);
+  #pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+              const uint32_t c = ct ? B24 : A24;
+              uint32_t e = (c & 0x3fu) | ((c << 2) & 0x3f00u) | ((c << 4) & 0x3f0000u) | ((c << 6) & 0x3f000000u);
+              e = (e & 0x1f1f1f1fu) | ((e & 0x20202020u) << 2);
+              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1));
+              xin[4 * ct + 0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 0) * lsc);
+              xin[4 * ct + 1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 1) * lsc);
+              xin[4 * ct + 2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 2) * lsc);
+              xin[4 * ct + 3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 3) * lsc);
+            }
+          } else {
+  #pragma unroll
+            for (int k = 0; k < 8; ++k) xin[k] = 0.f;
+          }
+  #pragma unroll
+          for (int ct = 0; ct < 2; ++ct) acc[(2 * bi + ct) * 8 + t] = (f32x4v){xin[4 * ct], xin[4 * ct + 1], xin[4 * ct + 2], xin[4 * ct + 3]};
+        } else {
+  #pragma unroll
+          for (int ct = 0; ct < 2; ++ct) acc[(2 * bi + ct) * 8 + t] = (f32x4v){0};
+        }
+        // hi / lo split, block keys: bf16 bits rounded up (>= the value) of max h, max |l|
+        float h[8], l[8], mh = 0.f, ml = 0.f;
+        f16x4 yh[2];
+  #pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const _Float16 hh = (_Float16)y[k];
+          yh[k >> 2][k & 3] = hh;
+          h[k] = (float)hh;
+          l[k] = y[k] - h[k];
+          mh = fmaxf(mh, h[k]);
+          ml = fmaxf(ml, fabsf(l[k]));
+        }
+        uint32_t key = (((__float_as_uint(mh) + 0xffffu) >> 16) << 16) | ((__float_as_uint(ml) + 0xffffu) >> 16);
+  #pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+          const uint32_t other = (uint32_t)__shfl_xor((int)key, o, 64);
+          key = (max(key >> 16, other >> 16) << 16) | max(key & 0xffffu, other & 0xffffu);
+        }
         if (valid) {
-          *reinterpret_cast<uint32_t*>(smem + baddr(term, bb, p, o32)) = w32;
-          *reinterpret_cast<uint16_t*>(smem + baddr(term, bb, p, o16)) = (uint16_t)w16;
-          if (g == 0) *reinterpret_cast<uint8_t*>(smem + baddr(term, bb, p, osc)) = (uint8_t)(127 + s);
+  #pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+            *reinterpret_cast<f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
+        }
+  #pragma unroll
+        for (int term = 0; term < 2; ++term) {
+          const uint32_t K = term ? key >> 16 : key & 0xffffu;
+          int s = (int)((K >> 7) & 0xffu) - 129 + ((K & 0x7fu) > 112u ? 1 : 0);
+          s = s < -120 ? -120 : s > 120 ? 120 : s;
+          const float f = __builtin_ldexpf(1.f, -s - 6);
+          const float* v = term ? h : l;
+          uint32_t c24[2];
+  #pragma unroll
+          for (int ct = 0; ct < 2; ++ct) {
+            uint32_t d = pk_fp8x4(v[4 * ct] * f, v[4 * ct + 1] * f, v[4 * ct + 2] * f, v[4 * ct + 3] * f);
+            d = (d & 0x1f1f1f1fu) | ((d >> 2) & 0x20202020u);
+            c24[ct] = (d & 0x3fu) | ((d >> 2) & 0xfc0u) | ((d >> 4) & 0x3f000u) | ((d >> 6) & 0xfc0000u);
+          }
+          const uint32_t P0 = c24[0] | (c24[1] << 24), P1 = c24[1] >> 8;
+          const uint32_t w32 = (g & 1) ? ((P0 >> 16) | (P1 << 16)) : P0;
+          const uint32_t w16 = (g & 1) ? (P0 & 0xffffu) : P1;
+          if (valid) {
+            *reinterpret_cast<uint32_t*>(smem + baddr(term, bb, p, o32)) = w32;
+            *reinterpret_cast<uint16_t*>(smem + baddr(term, bb, p, o16)) = (uint16_t)w16;
+            if (g == 0) *reinterpret_cast<uint8_t*>(smem + baddr(term, bb, p, osc)) = (uint8_t)(127 + s);
+          }
         }
       }
     }
@@ -641,6 +645,8 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
     hipLaunchKernelGGL((k_net_z<S, 8192 + 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var == 32768)
     hipLaunchKernelGGL((k_net_z<S, 32768>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 2048 + 8192)
+    hipLaunchKernelGGL((k_net_z<S, 2048 + 8192>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 8192)
     hipLaunchKernelGGL((k_net_z<S, 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var & 2048)
