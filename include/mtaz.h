@@ -132,7 +132,8 @@ int mtaz_stats(mtaz_engine* h, double* out, int n);
 /* record per-wave network HIP events during mtaz_play (trunk span for fp32, the fused
  * network kernel for fp16x3) */
 int mtaz_set_timing(mtaz_engine* h, int on);
-/* network arithmetic: 1 = fp16x3 split MFMA (default, fp32-accurate), 0 = fp32 MFMA */
+/* network arithmetic: 2 = k_net_z, f16 Wh*Xh + e4m3 cross terms (default, within 1e-5 of fp32),
+ * 1 = k_net_y, fp16x3 split MFMA (fp32-accurate to ~1e-8), 0 = fp32 MFMA */
 int mtaz_set_precision(mtaz_engine* h, int precision);
 /* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
 int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
@@ -141,7 +142,8 @@ int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
  * cycles, total 100 MHz ticks] from a separate diagnostic build (tools/bench_net.py) */
 int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int stamped, float* ms_out,
                   uint64_t* stamps_out);
-/* select a network kernel code variant for A/B timing (0 = the product kernel k_net_y) */
+/* select a network kernel code variant of the current precision for A/B timing (0 = the
+ * product kernel; the bits are listed in minitchess_alphazero_amd/engine.py set_net_variant) */
 int mtaz_set_net_variant(mtaz_engine* h, int variant);
 /* Two-network play (the arena of exp/learner.py:97-145): upload a network into weight slot 0
  * or 1 (mtaz_set_weights fills slot 0), and map agent 0 (the first mover, exp/agent.py:11-14)

@@ -322,10 +322,14 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
           ml = fmaxf(ml, fabsf(l[k]));
         }
         uint32_t key = (((__float_as_uint(mh) + 0xffffu) >> 16) << 16) | ((__float_as_uint(ml) + 0xffffu) >> 16);
-  #pragma unroll
-        for (int o = 16; o <= 32; o <<= 1) {
-          const uint32_t other = (uint32_t)__shfl_xor((int)key, o, 64);
-          key = (max(key >> 16, other >> 16) << 16) | max(key & 0xffffu, other & 0xffffu);
+        {
+          // max over the 4 lanes g of square n (lanes n + 16 g): v_permlane32_swap (lane i <->
+          // i + 32) then v_permlane16_swap (odd <-> even 16-lane rows), VALU ops instead of two
+          // dependent ds_bpermute round trips
+          const auto r32 = __builtin_amdgcn_permlane32_swap(key, key, false, false);
+          key = (max(r32[0] >> 16, r32[1] >> 16) << 16) | max(r32[0] & 0xffffu, r32[1] & 0xffffu);
+          const auto r16 = __builtin_amdgcn_permlane16_swap(key, key, false, false);
+          key = (max(r16[0] >> 16, r16[1] >> 16) << 16) | max(r16[0] & 0xffffu, r16[1] & 0xffffu);
         }
         if (valid) {
   #pragma unroll

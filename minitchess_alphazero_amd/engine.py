@@ -102,7 +102,8 @@ class Engine:
         """Select the network kernel code variant (0 = product) of the current precision.
         f16x3: 0 = k_net_y (v_mfma_f32_16x16x32_f16); NET_VAR_X (512) routes to k_net_x
         (32x32x16); the low bits pick A/B schedules of either kernel.  f16f8 (k_net_z):
-        2048 = 4 waves of 64 channels, 4096 = deeper prefetch, 8192 = e2m3 (fp6) cross terms,
+        2048 = 4 waves of 64 channels, 4096 = deeper prefetch, 8192 = e2m3 (fp6) cross terms
+        (10240 = both),
         262144 = ds_read_b64 operand reads, 524288 = per-row LDS swizzle table (8192 combines
         with the last two); 16384 / 32768 / 65536 / 131072 are timing-only diagnostic builds
         whose results are wrong by construction (k_net_z)."""
