@@ -31,7 +31,7 @@ NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3',
                'f16f8-deep': ('f16f8', 4096), 'f16f6': ('f16f8', 8192),
                'f16f8-r64': ('f16f8', 262144), 'f16f6-r64': ('f16f8', 270336),
                'f16f8-tbl': ('f16f8', 524288), 'f16f6-tbl': ('f16f8', 532480),
-               'f16f6-w4': ('f16f8', 10240)}
+               'f16f6-w4': ('f16f8', 10240), 'f16f8-prio': ('f16f8', 1048576)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
