@@ -50,6 +50,19 @@ __device__ __forceinline__ uint4 rd8x2(const char* p, int h) {
 }
 __device__ __forceinline__ f16x8 rd16x2(const char* p, int h) { return __builtin_bit_cast(f16x8, rd8x2(p, h)); }
 
+// f32(half of pk) * b + c in one v_fma_mix_f32 (the compiler does not form it with f32
+// denormals on); exact wherever the callers use it, so bit-identical to the unfused form
+__device__ __forceinline__ float zmix_lo(uint32_t pk, float b, float c) {
+  float r;
+  asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(pk), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float zmix_hi(uint32_t pk, float b, float c) {
+  float r;
+  asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(pk), "v"(b), "v"(c));
+  return r;
+}
+
 // 4 e4m3 bytes of {a, b, c, d} (round to nearest even, OCP e4m3fn)
 __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d) {
   int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
@@ -83,6 +96,9 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   // 1048576: static issue priority 1 for the second-dispatched half of the waves (the arbitration
   // loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
   constexpr bool PRIO = (VAR & 1048576) != 0;
+  // 2097152: the e4m3 epilogue's unfused form (product: v_fma_mix for the lo part, the Xh copy and
+  // the residual seed; bit-identical, test_gpu_net.py test_z_mix_epilogue_bit_identical)
+  constexpr bool NOMIX = (VAR & 2097152) != 0;
   __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
@@ -177,12 +193,20 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
           y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
           ymax[bb] = fmaxf(fmaxf(ymax[bb], fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
           if constexpr (conv_a) {
-            const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
             const int xl = *reinterpret_cast<const int*>(smem + al8);
-            a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[bb]);
-            a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[bb]);
-            a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[bb]);
-            a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[bb]);
+            if constexpr (NOMIX) {
+              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
+              a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[bb]);
+              a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[bb]);
+              a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[bb]);
+              a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[bb]);
+            } else {
+              const uint2 xp = *reinterpret_cast<const uint2*>(smem + ah);
+              a[0] = zmix_lo(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[bb]);
+              a[1] = zmix_hi(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[bb]);
+              a[2] = zmix_lo(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[bb]);
+              a[3] = zmix_hi(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[bb]);
+            }
           } else {
             a = (f32x4v){0};
           }
@@ -190,11 +214,25 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #pragma unroll
           for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
           float h[4], l[4];
+          if constexpr (NOMIX) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            h[j] = (float)yh[j];
-            l[j] = (y[j] - h[j]) * ls[bb];   // exact difference, power-of-two scale
-            h[j] *= hs[bb];
+            for (int j = 0; j < 4; ++j) {
+              h[j] = (float)yh[j];
+              l[j] = (y[j] - h[j]) * ls[bb];   // exact difference, power-of-two scale
+              h[j] *= hs[bb];
+            }
+          } else {
+            // l = y ls - h ls (= (y - h) ls, exact) and h hs straight from the packed halves
+            const uint2 yp = __builtin_bit_cast(uint2, yh);
+            const float nl = -ls[bb];
+            l[0] = zmix_lo(yp.x, nl, y[0] * ls[bb]);
+            l[1] = zmix_hi(yp.x, nl, y[1] * ls[bb]);
+            l[2] = zmix_lo(yp.y, nl, y[2] * ls[bb]);
+            l[3] = zmix_hi(yp.y, nl, y[3] * ls[bb]);
+            h[0] = zmix_lo(yp.x, hs[bb], 0.f);
+            h[1] = zmix_hi(yp.x, hs[bb], 0.f);
+            h[2] = zmix_lo(yp.y, hs[bb], 0.f);
+            h[3] = zmix_hi(yp.y, hs[bb], 0.f);
           }
           *reinterpret_cast<f16x4*>(smem + ah) = yh;
           *reinterpret_cast<uint32_t*>(smem + al8) = pk_fp8x4(l[0], l[1], l[2], l[3]);
@@ -635,7 +673,9 @@ template <bool S>
 static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
-  if (var == 1048576)
+  if (var == 2097152)
+    hipLaunchKernelGGL((k_net_z<S, 2097152>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+  else if (var == 1048576)
     hipLaunchKernelGGL((k_net_z<S, 1048576>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
   else if (var == 1048576 + 2048 + 8192)
     hipLaunchKernelGGL((k_net_z<S, 1048576 + 2048 + 8192>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);

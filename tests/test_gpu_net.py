@@ -137,6 +137,31 @@ def test_eight_wave_build_bit_identical(var):
     assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
 
 
+def test_z_mix_epilogue_bit_identical():
+    """k_net_z's product epilogue (v_fma_mix for the lo part, the e4m3 Xh copy and the residual
+    seed) stores the same values as the unfused form (variant 2097152): logits and values of the
+    two builds must be bitwise equal, on an ordinary and on a wide-range net."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from minitchess_alphazero_amd.network import Network
+    from tests_positions import random_fens
+    import torch
+    for net in (None, _wide_range_net()):
+        eng = Engine(n_games=64, sims=8)
+        eng.set_precision('f16f8')
+        if net is None:
+            torch.manual_seed(0)
+            net = Network()
+        eng.set_weights(net)
+        pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=7)])
+        eng.set_net_variant(0)
+        l0, v0 = eng.evaluate(pos)
+        eng.set_net_variant(2097152)
+        l1, v1 = eng.evaluate(pos)
+        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
 def _wide_range_net(gain=6.0):
     """Random-init net whose residual blocks amplify: both BatchNorm gammas of every block x
     `gain`, so the trunk's activations reach ~7e6 (f16's max is 65504)."""
