@@ -27,22 +27,81 @@ HBM_PEAK_GBS = 8000.0                # MI355X_MICROARCH.md HBM peak
 TREE_BYTES_PER_SIM = 700             # SURVEY 8d algorithmic bytes per simulation of the tree walk
 
 
-def cpu_baseline(sims, threads, seconds_cap):
-    """The oracle's restatement of the app/puppet CPU path (batch-1 torch-CPU fp32 per
-    leaf, FEN-keyed dict tables, Python rules), timed on this host: one full seeded game."""
+def _cpu_game(job):
+    """One seeded game of the oracle's restatement of the app/puppet CPU path (batch-1 torch-CPU
+    fp32 per leaf, FEN-keyed dict tables, Python rules) on `threads` torch threads."""
+    sims, seed, threads = job
     import torch
+    torch.set_num_threads(threads)
     from oracle.mcts import TorchNetEvaluator
     from oracle.net import seed0_network
     from oracle import selfplay
-    torch.set_num_threads(threads)
     ev = TorchNetEvaluator(seed0_network())
     st = {}
-    selfplay.play_games(ev, 1, sims, seed_base=0, stats=st)
-    s = st['seconds']
-    return {'value': 1.0 / s, 'unit': 'games/s', 'cores': threads, 'kind': 'port',
-            'sample': f'1 full self-play game (seed 0, {st["plies"]} plies, {sims} sims/move, {st["nn_evals"]} NN evals), '
-                      f'oracle restatement of app/puppet (batch-1 torch CPU fp32, dict tables, Python rules)',
-            'seconds': round(s, 3), 'sims_per_s': st['plies'] * sims / s, 'nn_evals_per_s': st['nn_evals'] / s}
+    selfplay.play_games(ev, 1, sims, seed_base=seed, stats=st)
+    return {'seconds': st['seconds'], 'plies': st['plies'], 'nn_evals': st['nn_evals']}
+
+
+def cpu_baseline(plan, all_threads, gpu_sims):
+    """seeded games (np.random.seed(g), random-init weights) at C1's 32 sims and
+    at the GPU's sims per move, each on all cores (games one after another, torch.set_num_threads =
+    all_threads) and on 1 thread (the games in parallel, one single-threaded process each: every
+    game still runs on exactly one core).  Children are separate processes (spawned, never
+    exec'ed over this one) and touch no GPU.  value = games/s at the GPU's sims on all cores."""
+    import multiprocessing as mp
+    seeds = [0, 1, 2] if plan == 'full' else [0]
+    sims_list = sorted({32, gpu_sims}) if plan == 'full' else [gpu_sims]
+    ctx = mp.get_context('spawn')
+    runs = {}
+    for sims in sims_list:
+        modes = [('all', all_threads)] + ([('1', 1)] if plan == 'full' else [])
+        for tag, thr in modes:
+            with ctx.Pool(len(seeds) if thr == 1 else 1) as pool:
+                games = pool.map(_cpu_game, [(sims, s, thr) for s in seeds], chunksize=1)
+            secs = [g['seconds'] for g in games]
+            runs[f'{sims}sims/{tag}'] = {
+                'threads': thr, 'seeds': seeds, 'seconds_per_game': [round(x, 3) for x in secs],
+                'games_per_s': len(secs) / sum(secs), 'plies': [g['plies'] for g in games],
+                'nn_evals': [g['nn_evals'] for g in games],
+                'sims_per_s': sum(g['plies'] for g in games) * sims / sum(secs)}
+    head = runs[f'{gpu_sims}sims/all']
+    return {'value': head['games_per_s'], 'unit': 'games/s', 'cores': all_threads, 'kind': 'port',
+            'sample': (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
+                       f'{gpu_sims} sims/move on {all_threads} threads: the oracle restatement of app/puppet '
+                       f'(batch-1 torch CPU fp32, dict tables, Python rules); value = games / total seconds'),
+            'sims_per_s': head['sims_per_s'], 'runs': runs}
+
+
+def kernel_roofline(tot, prec):
+    """Roofline of the dominant kernel from the engine's HIP events (one record per network launch).
+      f16f8 (default): k_net_z, the fused network with the fp16 split's two cross terms on the
+        block-scaled e4m3 MFMA (16x16x128);
+      f16x3: k_net_y, the same network with all three split products on f16 MFMA (16x16x32);
+        both: ONE launch per simulation wave = the whole network on the wave's leaves; algorithmic
+        FLOP per launch = leaves x 638,245,892 (SURVEY F3), peak = the dense f16 MFMA rate;
+      fp32: k_conv3x3, 18 launches per wave; FLOP per launch = leaves x 2*30*256*2304."""
+    from minitchess_alphazero_amd.engine import FLOP_PER_CONV_BOARD, FLOP_PER_EVAL
+    if prec in (1, 2):
+        launches = tot['waves']
+        flop_per_launch = FLOP_PER_EVAL * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
+        kernel, peak = 'k_net_y (fused network, fp16x3 on MFMA 16x16x32 f16)', F16_MATRIX_PEAK_TFLOPS
+        if prec == 2:
+            kernel = ('k_net_z (fused network: Wh*Xh on MFMA 16x16x32 f16, cross terms on the block-scaled '
+                      'e4m3 MFMA 16x16x128)')
+    else:
+        launches = 18 * tot['waves']
+        flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
+        kernel, peak = 'k_conv3x3 (fp32 MFMA 32x32x2)', FP32_MATRIX_PEAK_TFLOPS
+    passes_eq = {1: 3.0, 2: 2.0}.get(prec, 1.0)
+    ms = tot['trunk_ms'] / launches if launches else float('nan')
+    achieved = flop_per_launch / (ms * 1e-3) / 1e12
+    return {'bound': 'mfma', 'kernel': kernel, 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': achieved / peak, 'avg_launch_ms': ms, 'flop_per_launch': flop_per_launch,
+            'mfma_passes': {1: 'f16 x3', 2: 'f16 x1 + e4m3 x2'}.get(prec, 'f32 x1'),
+            # the MFMA work the split actually issues, in dense-f16 equivalents (an e4m3 MFMA of the
+            # block-scaled form runs at twice the f16 rate: 3 passes for f16x3, 1 + 2/2 for
+            # f16+e4m3), over the same dense f16 peak: the MFMA pipes' utilisation
+            'issued_achieved': achieved * passes_eq, 'issued_frac': achieved * passes_eq / peak}
 
 
 def main():
@@ -56,19 +115,31 @@ def main():
     ap.add_argument('--groups', type=int, default=1, help='game groups on separate HIP streams (mtaz_set_pipeline)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
+    ap.add_argument('--cpu-plan', default='full', choices=['full', 'quick'],
+                    help='full: BASELINE.md section 4 (3 seeded games x {32, --sims} sims x {all cores, 1 thread}); '
+                         'quick: 1 game at --sims on all cores')
+    ap.add_argument('--no-secondary', action='store_true',
+                    help='skip the second timed step with the fp32-accurate k_net_y (f16x3)')
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
-    ap.add_argument('--weights', default='', help='state_dict file (torch.save) instead of random init '
-                                                  '(BASELINE config 3: a checkpoint trained by the loop)')
+    ap.add_argument('--weights', default='', help='state_dict file (safetensors or torch.save) instead of random '
+                                                  'init (BASELINE config 3: tests/golden/c3/c3.safetensors)')
     ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
                     help='N>1 end-of-run reductions: nccl (RCCL, one GPU per rank) or gloo (host; with '
                          '--device, a rehearsal of the N-rank path on one GPU)')
     ap.add_argument('--device', type=int, default=None, help='GPU of this rank (default LOCAL_RANK)')
     args = ap.parse_args()
 
+    # N ranks: under torch.distributed.run WORLD_SIZE must equal --gpus; without a launcher this
+    # process starts the N ranks itself (before anything here touches the GPU) and exits with their code
+    from minitchess_alphazero_amd.launch import main_or_spawn
+    if os.environ.get('WORLD_SIZE') is None and args.gpus > 1:
+        from minitchess_alphazero_amd.build import build
+        build(verbose=False)                  # once for all ranks (hipcc only, no GPU call)
+    world = main_or_spawn(args.gpus, __file__)
+
     import numpy as np
     import torch
     rank = int(os.environ.get('RANK', 0))
-    world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
     dist = None
     device = local if args.device is None else args.device
@@ -88,7 +159,7 @@ def main():
         build(verbose=False)
     if dist is not None:
         dist.barrier()
-    from minitchess_alphazero_amd.engine import Engine, FLOP_PER_CONV_BOARD, FLOP_PER_EVAL, start_position
+    from minitchess_alphazero_amd.engine import Engine, FLOP_PER_EVAL, start_position
     from minitchess_alphazero_amd.network import Network
 
     from minitchess_alphazero_amd.sharding import reduce_run, shard
@@ -98,14 +169,18 @@ def main():
     weights_sha = None
     if args.weights:
         import hashlib
-        sd = torch.load(args.weights, map_location='cpu', weights_only=True)
-        h = hashlib.sha256()
-        for k, v in sd.items():
+        if args.weights.endswith('.safetensors'):
+            from safetensors.torch import load_file
+            sd = load_file(args.weights)
+        else:
+            sd = torch.load(args.weights, map_location='cpu', weights_only=True)
+        net = Network()
+        net.load_state_dict(sd)
+        h = hashlib.sha256()                      # over the state_dict in module order (tests/golden/c3.json)
+        for k, v in net.state_dict().items():
             h.update(k.encode())
             h.update(v.detach().cpu().contiguous().numpy().tobytes())
         weights_sha = h.hexdigest()
-        net = Network()
-        net.load_state_dict(sd)
         eng.set_weights(net)
     else:
         torch.manual_seed(0)                      # random-init weights of the reference architecture
@@ -134,43 +209,40 @@ def main():
     dt = time.perf_counter() - t0
     dt, tot = reduce_run(dt, tot, dist, red_device)
     games = G * args.steps * world
+    prec = int(st.get('net_precision', 0))
+
+    # secondary line: one more timed step on the fp32-accurate network (k_net_y, f16x3), same
+    # engine, seeds and workload, so both precisions' throughput comes from the same run
+    secondary = None
+    if not args.no_secondary and args.precision == 'f16f8':
+        eng.set_precision('f16x3')
+        eng.evaluate(np.stack([start_position()] * 8))    # load k_net_y's code object
+        sync()
+        t1 = time.perf_counter()
+        st2 = eng.play()
+        sync()
+        dt2 = time.perf_counter() - t1
+        tot2 = {k: st2[k] for k in tot}
+        dt2, tot2 = reduce_run(dt2, tot2, dist, red_device)
+        eng.set_precision(args.precision)
+        secondary = {'precision': 'f16x3 (fp16 hi/lo split, three f16 MFMA passes; fp32-accurate to ~1e-8)',
+                     'value': G * world / dt2, 'unit': 'games/s', 'steps': 1, 'ms_per_step': dt2 * 1e3,
+                     'sims_per_s': tot2['sims'] / dt2, 'roofline': kernel_roofline(tot2, 1)}
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    # roofline of the dominant kernel, timed with HIP events on the engine's stream:
-    #  f16f8 (default): k_net_z, as k_net_y below with the split's two cross terms on the
-    #    block-scaled e4m3 MFMA (16x16x128); algorithmic FLOP as below.
-    #  f16x3: k_net_y, ONE launch per simulation wave = the whole network on the
-    #    wave's leaves; algorithmic FLOP per launch = leaves x 638,245,892.
-    #    It runs on v_mfma_f32_16x16x32_f16, so the peak is the dense f16 MFMA rate; the 3
-    #    split passes mean issued MFMA FLOP = 3x the trunk's algorithmic FLOP.
-    #  fp32: k_conv3x3, 18 launches per wave; FLOP per launch = leaves x 2*30*256*2304.
-    prec = int(st.get('net_precision', 0))
-    f16x3 = prec in (1, 2)
-    if f16x3:
-        launches = tot['waves']
-        flop_per_launch = FLOP_PER_EVAL * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
-        kernel, peak = 'k_net_y (fused network, fp16x3 on MFMA 16x16x32 f16)', F16_MATRIX_PEAK_TFLOPS
-        if prec == 2:
-            kernel = ('k_net_z (fused network: Wh*Xh on MFMA 16x16x32 f16, cross terms on the block-scaled '
-                      'e4m3 MFMA 16x16x128)')
-    else:
-        launches = 18 * tot['waves']
-        flop_per_launch = FLOP_PER_CONV_BOARD * tot['trunk_boards'] / tot['waves'] if launches else float('nan')
-        kernel, peak = 'k_conv3x3 (fp32 MFMA 32x32x2)', FP32_MATRIX_PEAK_TFLOPS
-    passes_eq = {1: 3.0, 2: 2.0}.get(prec, 1.0)
-    conv_ms_avg = tot['trunk_ms'] / launches if launches else float('nan')
-    achieved = flop_per_launch / (conv_ms_avg * 1e-3) / 1e12
+    roof = kernel_roofline(tot, prec)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get('games') == args.games and tj.get('sims') == args.sims and kernel.startswith(tj.get('kernel', '?')):
+            if tj.get('games') == args.games and tj.get('sims') == args.sims and roof['kernel'].startswith(tj.get('kernel', '?')):
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
+    roof['traffic'] = traffic
     line = {
         'metric': METRIC,
         'value': games / dt,
@@ -183,8 +255,9 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': {1: 'f16x3 (fp16 hi/lo split, fp32 accumulate; fp32-accurate)',
-                  2: 'f16+e4m3 (fp16 hi/lo split; Wh*Xh in f16, cross terms in e4m3; fp32 accumulate; '
-                     'within 1e-5 of fp32)'}.get(prec, 'fp32'),
+                  2: 'f16+e4m3 (fp16 hi/lo split; Wh*Xh in f16, cross terms in e4m3; fp32 accumulate; priors and '
+                     'values within 1e-5 of the fp32 reference on the seed-0 and C3 nets, tests/test_gpu_search_parity.py)'
+                  }.get(prec, 'fp32'),
         'data': ('synthetic: self-play from STARTING_FEN, random-init weights (torch.manual_seed(0); Network())'
                  if not args.weights else f'synthetic: self-play from STARTING_FEN, trained checkpoint sha256 {weights_sha}'),
         'config': {'workload': (f'{G} parallel self-play games per GPU, {sims} sims/move, random-init policy net '
@@ -199,16 +272,7 @@ def main():
         'terminal_sims_per_game': tot['terminal_sims'] / games,
         'decisive_games': int(tot['decisive']),
         'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12,
-        'roofline': {'bound': 'mfma', 'kernel': kernel, 'achieved': achieved,
-                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
-                     'traffic': traffic, 'avg_launch_ms': conv_ms_avg, 'flop_per_launch': flop_per_launch,
-                     'mfma_passes': {1: 'f16 x3', 2: 'f16 x1 + e4m3 x2'}.get(prec, 'f32 x1'),
-                     # the MFMA work the split actually issues, in dense-f16 equivalents (an e4m3
-                     # MFMA of the block-scaled form runs at twice the f16 rate: 3 passes for
-                     # f16x3, 1 + 2/2 for f16+e4m3), over the same dense f16 peak: the MFMA
-                     # pipes' utilisation
-                     'issued_achieved': achieved * passes_eq,
-                     'issued_frac': achieved * passes_eq / peak},
+        'roofline': roof,
         # secondary roofline: the tree kernel k_select, HBM/latency-bound; algorithmic
         # bytes per simulation = SURVEY's estimate (path nodes: header + k edge reads + edge update,
         # leaf insert, hash probe, NN input) at k ~ 7.5, depth ~ 2
@@ -223,9 +287,11 @@ def main():
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
     }
+    if secondary is not None:
+        line['secondary'] = secondary
     if world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line['cpu_baseline'] = cpu_baseline(sims, threads, 120)
+        line['cpu_baseline'] = cpu_baseline(args.cpu_plan, threads, sims)
         line['vs_cpu_baseline'] = line['value'] / line['cpu_baseline']['value']
     print(json.dumps(line), flush=True)
     if dist is not None:

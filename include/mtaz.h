@@ -173,6 +173,13 @@ int mtaz_simulate(mtaz_engine* h, int first_sim, int n_sims);
 int mtaz_sim_select(mtaz_engine* h, int sim);
 int mtaz_leaves_get(mtaz_engine* h, int32_t* count, uint32_t* pos, int32_t* game, int32_t* k, uint16_t* codes);
 int mtaz_leaves_set(mtaz_engine* h, const float* P, const float* v, int count);
+/* the GPU network on the current leaf batch (what mtaz_simulate runs between select and backup):
+ * writes each leaf's priors P = softmax(logits[legal list]) and value v, the leaf evaluation of
+ * exp/agent.py:66-71 */
+int mtaz_sim_evaluate(mtaz_engine* h);
+/* read those device-written leaf results: P [count][KMAX] (first k entries of row i valid, the
+ * legal-list order of mtaz_leaves_get), v [count]; returns the leaf count (error if > count) */
+int mtaz_leaves_result(mtaz_engine* h, float* P, float* v, int count);
 int mtaz_sim_backup(mtaz_engine* h);
 /* root children codes and visit counts [n_games][kout] */
 int mtaz_move_end(mtaz_engine* h, uint16_t* codes, uint32_t* visits, int32_t* k, int kout);

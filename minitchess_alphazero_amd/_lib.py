@@ -70,6 +70,8 @@ SIGNATURES = {
     'mtaz_sim_select': (c_int, [c_void_p, c_int]),
     'mtaz_leaves_get': (c_int, [c_void_p, P_i32, P_u32, P_i32, P_i32, P_u16]),
     'mtaz_leaves_set': (c_int, [c_void_p, P_f32, P_f32, c_int]),
+    'mtaz_sim_evaluate': (c_int, [c_void_p]),
+    'mtaz_leaves_result': (c_int, [c_void_p, P_f32, P_f32, c_int]),
     'mtaz_sim_backup': (c_int, [c_void_p]),
     'mtaz_move_end': (c_int, [c_void_p, P_u16, P_u32, P_i32, c_int]),
     'mtaz_apply': (c_int, [c_void_p, P_i32]),

@@ -1,10 +1,11 @@
 """Build libmtaz.so (HIP for gfx950) in-tree with hipcc.
 
-Translation units: csrc/mtaz_device.hip (tree kernels + launchers), csrc/mtaz_net.hip
-and csrc/mtaz_net16.hip (network kernels), csrc/mtaz_host.cpp (C ABI, numpy-legacy RNG
-compiled with -ffp-contract=off, engine driver) and csrc/mtaz_wire.cpp (episode wire
-format).  The shared object lands next to this file so it travels to the
-GPU box with the repo snapshot.
+Translation units: csrc/mtaz_device.hip (tree kernels + launchers), csrc/mtaz_net16.hip and
+csrc/mtaz_net8.hip (network kernels k_net_y, k_net_z), csrc/mtaz_host.cpp (C ABI, numpy-legacy
+RNG compiled with -ffp-contract=off, engine driver) and csrc/mtaz_wire.cpp (episode wire
+format).  The shared object lands next to this file so it travels to the GPU box with the repo
+snapshot.  build(diag=True) makes libmtaz_diag.so with -DMTAZ_NET_DIAG: the network kernels'
+A/B and timing-only variants (tools/bench_net.py --diag), never loaded by the product path.
 """
 import os
 import subprocess
@@ -14,12 +15,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, 'libmtaz.so')
 BUILD = os.path.join(HERE, '_build')
+OUT_DIAG = os.path.join(HERE, 'libmtaz_diag.so')
+BUILD_DIAG = os.path.join(HERE, '_build_diag')
 INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
 ARCH = os.environ.get('MTAZ_OFFLOAD_ARCH', 'gfx950')
 
 SOURCES = [
     ('mtaz_device.hip', ['-O3']),
-    ('mtaz_net.hip', ['-O3']),
     ('mtaz_net16.hip', ['-O3']),
     ('mtaz_net8.hip', ['-O3']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
@@ -34,27 +36,30 @@ def _hipcc():
             return c
 
 
-def _stale():
-    if not os.path.exists(OUT):
+def _stale(out):
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     deps = [os.path.join(CSRC, s) for s, _ in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
     deps.append(os.path.join(INCLUDE, 'mtaz.h'))
     deps.append(os.path.abspath(__file__))
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
-        return OUT
-    os.makedirs(BUILD, exist_ok=True)
+def build(force=False, verbose=True, diag=False):
+    out, bdir = (OUT_DIAG, BUILD_DIAG) if diag else (OUT, BUILD)
+    if not force and not _stale(out):
+        return out
+    os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
     objs = []
     procs = []
     for src, flags in SOURCES:
-        obj = os.path.join(BUILD, src + '.o')
+        obj = os.path.join(bdir, src + '.o')
         cmd = [hipcc, '-x', 'hip', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-c',
                os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function'] + flags
+        if diag:
+            cmd.append('-DMTAZ_NET_DIAG')
         if verbose:
             print(' '.join(cmd), flush=True)
         procs.append((subprocess.Popen(cmd), cmd))
@@ -62,14 +67,14 @@ def build(force=False, verbose=True):
     for p, cmd in procs:
         if p.wait() != 0:
             raise RuntimeError('hipcc failed: ' + ' '.join(cmd))
-    tmp = OUT + '.tmp'
+    tmp = out + '.tmp'
     cmd = [hipcc, '-shared', f'--offload-arch={ARCH}', '-o', tmp] + objs + ['-lpthread']
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv)
+    build(force='--force' in sys.argv, diag='--diag' in sys.argv)

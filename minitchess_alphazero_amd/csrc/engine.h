@@ -112,20 +112,12 @@ struct NetWeights {
   const float* vl1_b;     // [256]
   const float* vl2_w;     // [256]
   const float* vl2_b;     // [1]
-  // fp16x3 trunk (k_net_x): per layer the BN-folded weights scaled by 2^e_L and split
-  // hi = f16(w), lo = f16(w - hi), laid out as the A operand of v_mfma_f32_32x32x16_f16:
-  // [L 18][cotile 8][kblock 144][part hi/lo][lane 64][8 x f16]; lane l holds
-  // W[co = 32*cotile + (l&31)][k = 16*kblock + 8*(l>>5) + j], k = tap*256 + ci.
-  const uint4* convx;
+  // fp16x3 trunk: per layer the BN-folded weights scaled by 2^e_L and split hi = f16(w),
+  // lo = f16(w - hi), as the A operand of v_mfma_f32_16x16x32_f16 (k_net_y; k_net_z reads the
+  // hi parts): [L 18][cotile 16][kblock 72][part][lane 64][8 x f16], lane l holds
+  // W[co = 16*cotile + (l&15)][k = 32*kblock + 8*(l>>4) + j], k = tap*256 + ci
   const float* convx_inv; // [18] 2^-e_L
-  // stem in the same form: K = 5 k-blocks of (2 taps x 8 channels), tap 9 = zero:
-  // [cotile 8][kblock 5][part][lane 64][8 x f16], lane l: co = 32*cotile + (l&31),
-  // tap = 2*kblock + (l>>5), channel j
-  const uint4* stemx;
-  const float* stemx_inv; // [1]
-  // the same split weights as the A operand of v_mfma_f32_16x16x32_f16 (k_net_y, product):
-  // [L 18][cotile 16][kblock 72][part][lane 64][8 x f16], lane l holds
-  // W[co = 16*cotile + (l&15)][k = 32*kblock + 8*(l>>4) + j]; scales as convx_inv
+  const float* stemx_inv; // [1] the stem's
   const uint4* convy;
   // stem: [cotile 16][kblock 3][part][lane 64][8 x f16], co = 16*cotile + (l&15),
   // tap = 4*kblock + (l>>4) (taps 9..11 zero), channel j; scale stemx_inv
@@ -158,7 +150,7 @@ struct NetWeights {
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
-constexpr size_t CONVX_U4_PER_LAYER = (size_t)8 * 144 * 2 * 64;  // 147,456 x 16 B = 2.36 MB
+constexpr size_t CONVX_U4_PER_LAYER = (size_t)16 * 72 * 2 * 64;  // 147,456 x 16 B = 2.36 MB (convy)
 enum NetPrecision { NET_FP32 = 0, NET_F16X3 = 1, NET_F16F8 = 2 };
 constexpr size_t CONV8_U4_PER_LAYER = (size_t)16 * 9 * 2 * 2 * 2 * 64;   // 73,728 x 16 B = 1.18 MB
 constexpr size_t CONV6_U4_PER_LAYER = (size_t)16 * 36 * 112;   // 64,512 x 16 B = 1.03 MB
@@ -185,22 +177,14 @@ void launch_move_begin(const Dev& d, hipStream_t s);
 void launch_select(const Dev& d, int sim, hipStream_t s);
 void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const Pos* pos, const int32_t* count, int max_b,
                 int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end);
-// fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup).
-// Product kernel: k_net_y on v_mfma_f32_16x16x32_f16 (mtaz_net16.hip).  Variant bit
-// NET_VAR_X selects k_net_x on v_mfma_f32_32x32x16_f16 (mtaz_net.hip); the low bits pick
-// A/B schedules of either kernel (tools/bench_net.py).
-constexpr int NET_VAR_X = 512;
+// fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup):
+// k_net_y on v_mfma_f32_16x16x32_f16 (mtaz_net16.hip)
 void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
                       float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
                       int variant);
 // diagnostic instantiation with per-phase s_memtime stamps (never the product path)
 void launch_net_f16x3_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
                               float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
-void launch_net_y(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
-                  float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
-                  int variant);
-void launch_net_y_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
-                          float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
 // k_net_z (mtaz_net8.hip): the same fused network with the split's cross terms Wh*Xl + Wl*Xh on
 // the block-scaled e4m3 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4), Wh*Xh on the f16 MFMA
 void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,

@@ -439,7 +439,8 @@ struct PlyRec {
 
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
-  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS, ST_COUNT
+  ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COUNT
 };
 
 template <class F>
@@ -503,7 +504,7 @@ struct mtaz_engine {
   NetBuffers nb{};
   bool weights_ok = false;
   int precision = NET_F16F8;   // k_net_z; NET_F16X3 = k_net_y (fp32-accurate to ~1e-8)
-  int variant = 0;   // fp16x3 network kernel variant (0 = product k_net_y; NET_VAR_X = k_net_x)
+  int variant = 0;   // network kernel variant of the current precision (0 = product; mtaz_set_net_variant)
   uint4* wxbuf = nullptr;
   float* wxinv = nullptr;
   float* wyrange = nullptr;
@@ -579,7 +580,7 @@ static int engine_alloc(mtaz_engine* h) {
   int hc = 1;
   while (hc < 2 * tr.NC) hc <<= 1;
   tr.HC = hc;
-  tr.EC = tr.NC * 16;
+  tr.EC = tr.NC * 24;   // average legal moves per expanded node <= 24 (trained nets reach 16+ at 256 sims)
   gm.DMAX = 2 * max_moves + 8;
   gm.HMAX = 2 * max_moves + 8;
   const size_t TN = (size_t)T * tr.NC, TE = (size_t)T * tr.EC;
@@ -808,7 +809,8 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.vl2_b = b + o_v2b;
 
   // fp16x3 trunk weights: per layer scale 2^e (max |w| * 2^e <= 8192), hi = f16(w),
-  // lo = f16(w - hi), in the A-operand order of v_mfma_f32_32x32x16_f16 (engine.h).
+  // lo = f16(w - hi); host staging in the 32x32x16 A-operand order (round 1's k_net_x), from
+  // which the 16x16x32 layouts below are gathered.
   std::vector<_Float16> wx((size_t)CONV_LAYERS * CONVX_U4_PER_LAYER * 8);
   std::vector<float> winv(CONV_LAYERS);
   for (int L = 0; L < CONV_LAYERS; ++L) {
@@ -993,7 +995,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   if (!h->wyrange) ECHK(h->dalloc(&h->wyrange, yr.size()));
   HIPCHK(hipMemcpy(h->wyrange, yr.data(), yr.size() * 4, hipMemcpyHostToDevice));
   h->w.yrange = h->wyrange;
-  const size_t nx = wx.size() / 8, ns = sx.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
+  const size_t nx = wy.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
   const size_t nsc = (sc8.size() + 3) / 4, n6 = w6.size() / 16;
   // half-swapped copies for the ds_read_b64 build (NetWeights::convz, conv8z)
   std::vector<_Float16> wz(wy);
@@ -1004,30 +1006,27 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   for (size_t u = 0; u < w8z.size() / 16; ++u)
     if (((u % 64) >> 4) & 1)
       for (int j = 0; j < 8; ++j) std::swap(w8z[u * 16 + j], w8z[u * 16 + 8 + j]);
-  const size_t oz = 2 * nx + ns + nsy + n8 + nsc + n6;
-  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, oz + nx + n8));
+  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6 | convz | conv8z
+  const size_t o_sy = nx, o_w8 = o_sy + nsy, o_sc = o_w8 + n8, o_w6 = o_sc + nsc, o_z = o_w6 + n6;
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, o_z + nx + n8));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
-  HIPCHK(hipMemcpy(h->wxbuf, wx.data(), nx * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + nx, sx.data(), ns * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + nx + ns, wy.data(), nx * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns, sy.data(), nsy * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy, w8.data(), n8 * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy + n8, sc8.data(), sc8.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + 2 * nx + ns + nsy + n8 + nsc, w6.data(), n6 * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + oz, wz.data(), nx * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + oz + nx, w8z.data(), n8 * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf, wy.data(), nx * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_sy, sy.data(), nsy * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_w8, w8.data(), n8 * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_sc, sc8.data(), sc8.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_w6, w6.data(), n6 * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_z, wz.data(), nx * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_z + nx, w8z.data(), n8 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
-  h->w.convx = h->wxbuf;
   h->w.convx_inv = h->wxinv;
-  h->w.stemx = h->wxbuf + nx;
   h->w.stemx_inv = h->wxinv + CONV_LAYERS;
-  h->w.convy = h->wxbuf + nx + ns;
-  h->w.stemy = h->wxbuf + 2 * nx + ns;
-  h->w.conv8 = h->wxbuf + 2 * nx + ns + nsy;
-  h->w.conv8_sc = reinterpret_cast<const int32_t*>(h->wxbuf + 2 * nx + ns + nsy + n8);
-  h->w.conv6 = h->wxbuf + 2 * nx + ns + nsy + n8 + nsc;
-  h->w.convz = h->wxbuf + oz;
-  h->w.conv8z = h->wxbuf + oz + nx;
+  h->w.convy = h->wxbuf;
+  h->w.stemy = h->wxbuf + o_sy;
+  h->w.conv8 = h->wxbuf + o_w8;
+  h->w.conv8_sc = reinterpret_cast<const int32_t*>(h->wxbuf + o_sc);
+  h->w.conv6 = h->wxbuf + o_w6;
+  h->w.convz = h->wxbuf + o_z;
+  h->w.conv8z = h->wxbuf + o_z + nx;
   h->weights_ok = true;
   return 0;
 }
@@ -1089,7 +1088,20 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   return check_err(h);
 }
 
+// Variants a product library accepts: each parity-green against the reference fixtures
+// (tests/test_gpu_net.py).  k_net_y: 1024 = unfused epilogue (bit-identity reference).  k_net_z:
+// 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms.  The
+// timing-only diagnostic builds (wrong results by construction) exist only in a library built
+// with MTAZ_NET_DIAG (tools/bench_net.py --diag).
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
+  bool ok = variant == 0;
+  if (h->precision == NET_F16X3) ok = ok || variant == 1024;
+  if (h->precision == NET_F16F8) ok = ok || variant == 2097152 || variant == 8192;
+#ifdef MTAZ_NET_DIAG
+  ok = true;
+#endif
+  if (!ok) return set_err(MTAZ_E_FAIL, "network variant %d is not a parity-tested build of precision %d", variant,
+                          h->precision);
   h->variant = variant;
   return 0;
 }
@@ -1144,6 +1156,7 @@ extern "C" int mtaz_set_precision(mtaz_engine* h, int precision) {
   if (precision != NET_FP32 && precision != NET_F16X3 && precision != NET_F16F8)
     return set_err(MTAZ_E_FAIL, "precision must be 0 (fp32), 1 (fp16x3) or 2 (f16 + e4m3 cross terms)");
   h->precision = precision;
+  h->variant = 0;   // variants are per precision
   return 0;
 }
 
@@ -1300,6 +1313,28 @@ extern "C" int mtaz_leaves_set(mtaz_engine* h, const float* P, const float* v, i
   }
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
+}
+
+extern "C" int mtaz_sim_evaluate(mtaz_engine* h) {
+  if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
+  HIPCHK(hipSetDevice(h->device));
+  launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  return check_err(h);
+}
+
+extern "C" int mtaz_leaves_result(mtaz_engine* h, float* P, float* v, int count) {
+  HIPCHK(hipSetDevice(h->device));
+  int32_t c = 0;
+  HIPCHK(hipMemcpyAsync(&c, h->d.lf.count, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (count < c) return set_err(MTAZ_E_CAPACITY, "leaf batch holds %d leaves, buffer %d", c, count);
+  if (c > 0) {
+    HIPCHK(hipMemcpyAsync(P, h->d.lf.P, (size_t)c * KMAX * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(v, h->d.lf.v, c * 4, hipMemcpyDeviceToHost, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return c;
 }
 
 extern "C" int mtaz_sim_backup(mtaz_engine* h) {
@@ -1563,10 +1598,13 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     plies += (int64_t)h->rec[g].size();
     decisive += h->final_outcome[g] == DECISIVE;
   }
-  int32_t mxn = 0;
-  for (int t = 0; t < 2 * n_games && t < 64; ++t) {
-    int32_t nn, ne;
-    if (mtaz_tree_size(h, t, &nn, &ne) == 0) mxn = std::max(mxn, nn);
+  // largest table of the batch (device error flags already guard the capacities)
+  int32_t mxn = 0, mxe = 0;
+  {
+    std::vector<int32_t> nn(2 * n_games), ne(2 * n_games);
+    HIPCHK(hipMemcpy(nn.data(), h->d.tr.n_nodes, nn.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ne.data(), h->d.tr.n_edges, ne.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t t = 0; t < nn.size(); ++t) mxn = std::max(mxn, nn[t]), mxe = std::max(mxe, ne[t]);
   }
   h->stats[ST_PLIES] = (double)plies;
   h->stats[ST_NN_EVALS] = evals;
@@ -1581,6 +1619,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_MOVES] = moves;
   h->stats[ST_TRUNK_LAUNCHES] = h->timing ? 18.0 * h->wave : 0;
   h->stats[ST_MAX_NODES] = mxn;
+  h->stats[ST_MAX_EDGES] = mxe;
   h->stats[ST_SYNC_MS] = sync_ms;
   h->stats[ST_NET_PREC] = h->precision;
   h->stats[ST_SELECT_MS] = select_ms;
@@ -1588,6 +1627,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
 }
 
 extern "C" int mtaz_stats(mtaz_engine* h, double* out, int n) {
+  h->stats[ST_NODE_CAP] = h->d.tr.NC;   // per-table capacities (engine_alloc)
+  h->stats[ST_EDGE_CAP] = h->d.tr.EC;
   for (int i = 0; i < n && i < ST_COUNT; ++i) out[i] = h->stats[i];
   return ST_COUNT;
 }

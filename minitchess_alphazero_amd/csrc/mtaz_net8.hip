@@ -51,7 +51,11 @@ __device__ __forceinline__ uint4 rd8x2(const char* p, int h) {
 __device__ __forceinline__ f16x8 rd16x2(const char* p, int h) { return __builtin_bit_cast(f16x8, rd8x2(p, h)); }
 
 // f32(half of pk) * b + c in one v_fma_mix_f32 (the compiler does not form it with f32
-// denormals on); exact wherever the callers use it, so bit-identical to the unfused form
+// denormals on).  Bit-identical to the unfused form (round the product, then add) where the
+// product f32(half) * b is exact and neither it, c nor the sum is an f32 denormal or overflows:
+// the callers' b are powers of two and the operands are normal-range activations (a denormal
+// sum would be flushed differently by the mix path); test_z_mix_epilogue_bit_identical checks
+// ordinary and wide-range nets
 __device__ __forceinline__ float zmix_lo(uint32_t pk, float b, float c) {
   float r;
   asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(pk), "v"(b), "v"(c));
@@ -673,42 +677,31 @@ template <bool S>
 static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetWeights& w, const Pos* pos,
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
-  if (var == 2097152)
-    hipLaunchKernelGGL((k_net_z<S, 2097152>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 1048576)
-    hipLaunchKernelGGL((k_net_z<S, 1048576>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 1048576 + 2048 + 8192)
-    hipLaunchKernelGGL((k_net_z<S, 1048576 + 2048 + 8192>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 524288)
-    hipLaunchKernelGGL((k_net_z<S, 524288>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 524288 + 8192)
-    hipLaunchKernelGGL((k_net_z<S, 524288 + 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 262144)
-    hipLaunchKernelGGL((k_net_z<S, 262144>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 262144 + 8192)
-    hipLaunchKernelGGL((k_net_z<S, 262144 + 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 16384)
-    hipLaunchKernelGGL((k_net_z<S, 16384>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 65536)
-    hipLaunchKernelGGL((k_net_z<S, 65536>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 131072)
-    hipLaunchKernelGGL((k_net_z<S, 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 65536 + 131072)
-    hipLaunchKernelGGL((k_net_z<S, 65536 + 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 8192 + 131072)
-    hipLaunchKernelGGL((k_net_z<S, 8192 + 131072>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 32768)
-    hipLaunchKernelGGL((k_net_z<S, 32768>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var == 2048 + 8192)
-    hipLaunchKernelGGL((k_net_z<S, 2048 + 8192>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var & 8192)
-    hipLaunchKernelGGL((k_net_z<S, 8192>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var & 2048)
-    hipLaunchKernelGGL((k_net_z<S, 2048>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else if (var & 4096)
-    hipLaunchKernelGGL((k_net_z<S, 4096>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
-  else
-    hipLaunchKernelGGL((k_net_z<S, 0>), grid, dim3(512), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+#define Z_LAUNCH(V, T)                                                                                       \
+  hipLaunchKernelGGL((k_net_z<S, V>), grid, dim3(T), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps)
+  // product builds (mtaz_set_net_variant accepts these): 0, the unfused epilogue, e2m3 cross terms
+  if (var == 2097152) Z_LAUNCH(2097152, 512);
+  else if (var == 8192) Z_LAUNCH(8192, 512);
+#ifdef MTAZ_NET_DIAG
+  // A/B and timing-only builds: the diagnostic library only (tools/bench_net.py --diag)
+  else if (var == 1048576) Z_LAUNCH(1048576, 512);
+  else if (var == 1048576 + 2048 + 8192) Z_LAUNCH(1048576 + 2048 + 8192, 256);
+  else if (var == 524288) Z_LAUNCH(524288, 512);
+  else if (var == 524288 + 8192) Z_LAUNCH(524288 + 8192, 512);
+  else if (var == 262144) Z_LAUNCH(262144, 512);
+  else if (var == 262144 + 8192) Z_LAUNCH(262144 + 8192, 512);
+  else if (var == 16384) Z_LAUNCH(16384, 512);
+  else if (var == 32768) Z_LAUNCH(32768, 512);
+  else if (var == 65536) Z_LAUNCH(65536, 512);
+  else if (var == 131072) Z_LAUNCH(131072, 512);
+  else if (var == 65536 + 131072) Z_LAUNCH(65536 + 131072, 512);
+  else if (var == 8192 + 131072) Z_LAUNCH(8192 + 131072, 512);
+  else if (var == 2048 + 8192) Z_LAUNCH(2048 + 8192, 256);
+  else if (var == 2048) Z_LAUNCH(2048, 256);
+  else if (var == 4096) Z_LAUNCH(4096, 512);
+#endif
+  else Z_LAUNCH(0, 512);
+#undef Z_LAUNCH
 }
 
 void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,

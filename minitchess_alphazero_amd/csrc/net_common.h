@@ -1,6 +1,6 @@
-// Pieces shared by the fused fp16x3 network kernels (k_net_x: v_mfma_f32_32x32x16_f16,
-// mtaz_net.hip; k_net_y: v_mfma_f32_16x16x32_f16, mtaz_net16.hip): the LDS activation image,
-// the stem input, and the policy/value heads (exp/policy.py:62-80, exp/agent.py:67-69).
+// Pieces shared by the fused network kernels (k_net_y: fp16x3 on v_mfma_f32_16x16x32_f16,
+// mtaz_net16.hip; k_net_z: f16 + e4m3 cross terms, mtaz_net8.hip): the LDS activation image, the
+// stem input, and the policy/value heads (exp/policy.py:62-80, exp/agent.py:67-69).
 #pragma once
 #include "engine.h"
 

@@ -24,9 +24,8 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
-              'select_ms']
+              'select_ms', 'node_cap', 'edge_cap']
 
-NET_VAR_X = 512   # mtaz_set_net_variant bit: k_net_x (v_mfma_f32_32x32x16_f16) instead of k_net_y
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
 # one trunk conv on one board: 30 positions x 256 out x 2304 K, 2 FLOP/MAC
@@ -99,14 +98,11 @@ class Engine:
         _lib.check(self.L.mtaz_set_precision(self.h, {'fp32': 0, 'f16x3': 1, 'f16f8': 2}[precision]))
 
     def set_net_variant(self, variant):
-        """Select the network kernel code variant (0 = product) of the current precision.
-        f16x3: 0 = k_net_y (v_mfma_f32_16x16x32_f16); NET_VAR_X (512) routes to k_net_x
-        (32x32x16); the low bits pick A/B schedules of either kernel.  f16f8 (k_net_z):
-        2048 = 4 waves of 64 channels, 4096 = deeper prefetch, 8192 = e2m3 (fp6) cross terms
-        (10240 = both),
-        262144 = ds_read_b64 operand reads, 524288 = per-row LDS swizzle table (8192 combines
-        with the last two); 16384 / 32768 / 65536 / 131072 are timing-only diagnostic builds
-        whose results are wrong by construction (k_net_z)."""
+        """Select a parity-tested build of the current precision's network kernel (0 = product;
+        set_precision resets it).  f16x3 (k_net_y): 1024 = the epilogue in unfused form.  f16f8
+        (k_net_z): 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross terms.  Other
+        values are rejected; the A/B and timing-only diagnostic builds exist only in
+        libmtaz_diag.so (MTAZ_LIB, tools/bench_net.py --diag)."""
         _lib.check(self.L.mtaz_set_net_variant(self.h, int(variant)))
 
     def set_pipeline(self, groups):
@@ -245,6 +241,18 @@ class Engine:
         if c == 0:
             vv = np.zeros(1, np.float32)
         _lib.check(self.L.mtaz_leaves_set(self.h, _p(P, ctypes.c_float), _p(vv, ctypes.c_float), c))
+
+    def sim_evaluate(self):
+        """The GPU network on the current leaf batch (select -> evaluate -> backup = simulate)."""
+        _lib.check(self.L.mtaz_sim_evaluate(self.h))
+
+    def leaf_results(self):
+        """Device-written leaf priors and values of the last sim_evaluate: (P [c, KMAX] float32,
+        row i's first k[i] entries valid in legal-list order; v [c] float32)."""
+        P = np.zeros((self.G, _lib.KMAX), np.float32)
+        v = np.zeros(self.G, np.float32)
+        c = _lib.check(self.L.mtaz_leaves_result(self.h, _p(P, c_float), _p(v, c_float), self.G))
+        return P[:c], v[:c]
 
     def sim_backup(self):
         _lib.check(self.L.mtaz_sim_backup(self.h))

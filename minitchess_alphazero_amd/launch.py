@@ -1,0 +1,74 @@
+"""One process per GPU without an external launcher.
+
+`python bench.py --gpus N` (the driver's form) must run N ranks even when nothing like
+torch.distributed.run started it.  spawn_ranks() starts N children of the same command line with
+the launcher's environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT) and waits for
+them.  The parent never initialises HIP: it must be called before anything in the calling process
+touches the GPU (no torch.cuda call, no engine), and it starts the children as new processes
+(subprocess), never by replacing itself.  This module imports no torch.
+"""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv, env=None, poll_s=0.2):
+    """Run `argv` as ranks 0..n-1 (children inherit stdout/stderr) and return the exit code: 0 if
+    every rank exits 0, else the first non-zero code seen.  When a rank fails, the others are
+    terminated (then killed after 30 s) so that no rank waits forever in a collective."""
+    if n < 1:
+        raise ValueError(f'need at least one rank, got {n}')
+    base = dict(os.environ if env is None else env)
+    base.setdefault('MASTER_ADDR', '127.0.0.1')
+    base['MASTER_PORT'] = str(free_port())
+    base['WORLD_SIZE'] = str(n)
+    base['LOCAL_WORLD_SIZE'] = str(n)
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(list(argv), env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(poll_s)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 30
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+    return rc
+
+
+def main_or_spawn(n_requested, script):
+    """For a script started as `python script ... --gpus N`: returns the world size this process
+    belongs to, after checking it against N, or (with no launcher and N > 1) runs N ranks of the
+    same command line and exits with their code."""
+    world_env = os.environ.get('WORLD_SIZE')
+    if world_env is None and n_requested > 1:
+        sys.exit(spawn_ranks(n_requested, [sys.executable, os.path.abspath(script)] + sys.argv[1:]))
+    world = int(world_env or 1)
+    if world != n_requested:
+        sys.stderr.write(f'{os.path.basename(script)}: --gpus {n_requested} but the launcher started '
+                         f'{world} rank(s) (WORLD_SIZE)\n')
+        sys.exit(2)
+    return world

@@ -77,13 +77,15 @@ class SyntheticEvaluator:
 class MonteCarloTreeSearch:
     """exp/agent.py:24-88 (FEN-keyed transposition DAG)."""
 
-    def __init__(self, environment, evaluator, cpuct, rng=None, cast_mode=2, record=None):
+    def __init__(self, environment, evaluator, cpuct, rng=None, cast_mode=2, record=None, trace=None):
         self._environment = environment
         self._evaluator = evaluator
         self._cpuct = cpuct
         self._rng = rng if rng is not None else np.random.mtrand._rand
         self._cast_mode = cast_mode
         self._record = record
+        # test instrumentation: every PUCT selection as (node, u, chosen index, N.sum())
+        self._trace = trace
         self._data = {'Q': {}, 'N': {}, 'P': {}, 'terminal': {}, 'visited': set(), 'legal_moves': {}}
         self.nn_evals = 0
         self.terminal_hits = 0
@@ -105,7 +107,7 @@ class MonteCarloTreeSearch:
             Q[action] = (N[action] * Q[action] + value) / (N[action] + 1)
             N[action] += 1
 
-    def _puct(self, Q, N, P, root):                                                # :79-85
+    def _puct(self, Q, N, P, root, node=None):                                     # :79-85
         if root:
             k = len(Q)
             P = 0.75 * P + 0.25 * self._rng.dirichlet([0.6] * k)                 # :81-82
@@ -117,7 +119,10 @@ class MonteCarloTreeSearch:
         else:
             t = cp * s
         u = Q + t / (1 + N)
-        return u.argmax()
+        a = u.argmax()
+        if self._trace is not None:
+            self._trace.append((node, u.copy(), int(a), float(N.sum())))
+        return a
 
     def _search(self, episode, chain):                                             # :54-88
         d = self._data
@@ -148,7 +153,7 @@ class MonteCarloTreeSearch:
                 return
             Q, N, P = d['Q'][node], d['N'][node], d['P'][node]
             legal_moves = d['legal_moves'][node]
-            action = self._puct(Q, N, P, len(chain) == 0)
+            action = self._puct(Q, N, P, len(chain) == 0, node)
             episode.step(legal_moves[action], return_status=False)
             chain.append((node, action))
 
@@ -185,7 +190,7 @@ class SimpleAlphaZeroAgent:
     """exp/agent.py:91-119."""
 
     def __init__(self, environment, policy, num_simulations, cpuct=1, tau_change=6,
-                 rng=None, cast_mode=2, record=None):
+                 rng=None, cast_mode=2, record=None, trace=None):
         self._environment = environment
         self.policy = policy
         self._num_simulations = num_simulations
@@ -194,11 +199,13 @@ class SimpleAlphaZeroAgent:
         self._rng = rng if rng is not None else np.random.mtrand._rand
         self._cast_mode = cast_mode
         self._record = record
+        self._trace = trace
         self.init_mcts()
 
     def init_mcts(self):
         self._mcts = MonteCarloTreeSearch(self._environment, self.policy.model, self._cpuct,
-                                          rng=self._rng, cast_mode=self._cast_mode, record=self._record)
+                                          rng=self._rng, cast_mode=self._cast_mode, record=self._record,
+                                          trace=self._trace)
 
     @property
     def mcts(self):

@@ -79,7 +79,7 @@ class _MCInit:
 
 
 def play_games(evaluator, num_games, sims, seed_base=0, cpuct=1, tau_change=6, cast_mode=2,
-               record=None, stats=None):
+               record=None, stats=None, trace=None):
     """Play `num_games` seeded self-play games; return the list of episode records.
     `evaluator` may be a pair: agent 0 (first mover, exp/agent.py:11-14) uses the first, agent 1
     the second (the arena of the commented exp/learner.py:97-145)."""
@@ -87,7 +87,7 @@ def play_games(evaluator, num_games, sims, seed_base=0, cpuct=1, tau_change=6, c
     rng = np.random.RandomState(seed_base)
     evs = tuple(evaluator) if isinstance(evaluator, (tuple, list)) else (evaluator, evaluator)
     agents = [SimpleAlphaZeroAgent(env, SimpleAlphaZeroPolicy(evs[i]), sims, cpuct, tau_change, rng=rng,
-                                   cast_mode=cast_mode, record=record) for i in range(2)]
+                                   cast_mode=cast_mode, record=record, trace=trace) for i in range(2)]
     sink = []
     referee = RoundRobinReferee(agents)
     callbacks = [InfoRecorder(sink), _MCInit(agents[0]), _MCInit(agents[1])]

@@ -12,8 +12,14 @@ import numpy as np
 from minitchess_alphazero_amd.environment import STARTING_FEN, pos_to_fen
 
 
-def drive_engine(eng, n_games, sims, seeds, evaluator=None, tau=6, start_fen=STARTING_FEN, trees_out=None):
-    eng.set_games([start_fen] * n_games)
+def drive_engine(eng, n_games, sims, seeds, evaluator=None, tau=6, start_fen=STARTING_FEN, trees_out=None,
+                 capture=None):
+    """start_fen: one FEN for every game, or a list with one per game.  With the GPU network
+    (evaluator=None) and a dict `capture`, each simulation runs as sim_select -> sim_evaluate ->
+    sim_backup (the kernels of simulate()) and capture[fen] = (P, v) records the network's
+    device-written leaf results."""
+    starts = [start_fen] * n_games if isinstance(start_fen, str) else list(start_fen)
+    eng.set_games(starts)
     eng.clear_trees()
     rngs = [np.random.RandomState(s) for s in seeds]
     recs = [[] for _ in range(n_games)]
@@ -31,7 +37,15 @@ def drive_engine(eng, n_games, sims, seeds, evaluator=None, tau=6, start_fen=STA
                 noise.append(None)
         eng.set_noise(noise)
         for s in range(sims):
-            if evaluator is None:
+            if evaluator is None and capture is not None:
+                eng.sim_select(s)
+                lpos, _lg, lk, _lc = eng.leaves()
+                eng.sim_evaluate()
+                P, v = eng.leaf_results()
+                for i in range(len(lk)):
+                    capture[pos_to_fen(lpos[i])] = (P[i][:lk[i]].copy(), float(v[i]))
+                eng.sim_backup()
+            elif evaluator is None:
                 eng.simulate(s, 1)
             else:
                 eng.sim_select(s)
@@ -91,3 +105,61 @@ def compare_records(got, ref):
     if len(got) != len(ref) and first is None:
         first = n
     return same, max(len(got), len(ref)), first
+
+
+def c3_network():
+    """BASELINE config 3's checkpoint (tests/golden/make_golden_r2.py), sha256-checked."""
+    import json
+    import os
+    from safetensors.torch import load_file
+    from minitchess_alphazero_amd.network import Network
+    from oracle.net import state_dict_sha256
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+    net = Network()
+    net.load_state_dict(load_file(os.path.join(here, 'c3', 'c3.safetensors')))
+    meta = json.load(open(os.path.join(here, 'c3.json')))
+    assert state_dict_sha256(net) == meta['state_dict_sha256'], 'C3 checkpoint does not match its pinned sha256'
+    return net.eval()
+
+
+class RecordedEvaluator:
+    """Oracle evaluator returning recorded leaf results by FEN (the network is a function of the
+    position, so a replay asks only for positions the recorded run evaluated)."""
+
+    def __init__(self, table):
+        self.table = table
+
+    def evaluate(self, fen, legal_moves):
+        P, v = self.table[fen]
+        assert len(P) == len(legal_moves), fen
+        return np.asarray(P, np.float32), v
+
+
+def explain_divergence(gpu_leaves, ref_evaluator, sims, seed, gpu_moves, prior_tol=1e-5, value_tol=1e-5):
+    """Why a GPU-network game left the reference game.  Two oracle replays of game `seed`, one with
+    the GPU's recorded leaf results (it must reproduce the GPU game exactly) and one with the
+    reference network, record every PUCT selection; the first selection where they differ is the
+    flip.  Returns the reference's decision margin there (u of its choice - u of the GPU's choice),
+    the GPU run's opposite margin, and the largest margin the north_star tolerance allows:
+    priors within prior_tol and values within value_tol move u = Q + cpuct*P'*sqrt(S)/(1+N) of a
+    child by at most value_tol + prior_tol*sqrt(S) (Q is an average of backed-up values; the root
+    noise mix scales P by 0.75), so a flip between two children is explained by the tolerance when
+    margin_ref + margin_gpu <= 2*(value_tol + prior_tol*sqrt(S))."""
+    from oracle import selfplay
+    tr_gpu, tr_ref = [], []
+    rec_gpu = selfplay.play_games(RecordedEvaluator(gpu_leaves), 1, sims, seed_base=seed, trace=tr_gpu)[0]
+    same, _total, first = compare_records(rec_gpu, gpu_moves)
+    assert first is None, f'the oracle replay of the GPU leaves left the GPU game at ply {first}'
+    selfplay.play_games(ref_evaluator, 1, sims, seed_base=seed, trace=tr_ref)
+    for i, (a, b) in enumerate(zip(tr_ref, tr_gpu)):
+        if a[0] != b[0] or a[2] != b[2]:
+            assert a[0] == b[0], 'the replays reached different nodes without a differing selection'
+            u_ref, u_gpu, ar, ag = a[1], b[1], a[2], b[2]
+            S = a[3]
+            m_ref = float(u_ref[ar] - u_ref[ag])
+            m_gpu = float(u_gpu[ag] - u_gpu[ar])
+            bound = 2 * (value_tol + prior_tol * np.sqrt(S))
+            return {'selection': i, 'node': a[0], 'ref_choice': ar, 'gpu_choice': ag, 'visits_at_node': S,
+                    'margin_ref': m_ref, 'margin_gpu': m_gpu, 'tolerance_bound': float(bound),
+                    'explained': bool(m_ref >= 0 and m_gpu >= 0 and m_ref + m_gpu <= bound)}
+    return None

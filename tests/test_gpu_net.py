@@ -23,15 +23,9 @@ def _softmax(x):
     return e / e.sum()
 
 
-# f16x3 = product fused kernel k_net_y (16x16x32 MFMA) and its A/B schedules (4, 8, 128);
-# f16x3-x* = k_net_x (32x32x16 MFMA, variant bit 512) and its schedules; fp32 = fp32 MFMA path
-NET_KERNELS = {'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0), 'f16x3-y4': ('f16x3', 4), 'f16x3-y128': ('f16x3', 128),
-               'f16x3-y8': ('f16x3', 8), 'f16x3-x': ('f16x3', 512), 'f16x3-y2048': ('f16x3', 2048),
-               'f16x3-y6144': ('f16x3', 6144), 'f16f8': ('f16f8', 0), 'f16f8-w4': ('f16f8', 2048),
-               'f16f8-deep': ('f16f8', 4096), 'f16f6': ('f16f8', 8192),
-               'f16f8-r64': ('f16f8', 262144), 'f16f6-r64': ('f16f8', 270336),
-               'f16f8-tbl': ('f16f8', 524288), 'f16f6-tbl': ('f16f8', 532480),
-               'f16f6-w4': ('f16f8', 10240), 'f16f8-prio': ('f16f8', 1048576)}
+# every build the product library accepts (mtaz_set_net_variant): f16f8 = k_net_z (default),
+# f16f6 = k_net_z with e2m3 cross terms, f16x3 = k_net_y, fp32 = the fp32 MFMA path
+NET_KERNELS = {'f16f8': ('f16f8', 0), 'f16f6': ('f16f8', 8192), 'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
@@ -115,26 +109,20 @@ def test_mix_epilogue_bit_identical():
     assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
 
 
-@pytest.mark.parametrize('var', [2048, 6144])
-def test_eight_wave_build_bit_identical(var):
-    """The 8-wave build (2 waves per SIMD, 32 output channels per wave) issues every
-    accumulator's MFMAs in the product's order, so its logits and values are bitwise equal."""
+def test_product_library_rejects_untested_variants():
+    """Only parity-tested builds are selectable; the timing-only diagnostic variants (wrong results
+    by construction) are not in the product library."""
+    from minitchess_alphazero_amd import _lib
     from minitchess_alphazero_amd.engine import Engine
-    from minitchess_alphazero_amd.environment import pos_from_fen
-    from minitchess_alphazero_amd.network import Network
-    from tests_positions import random_fens
-    import torch
-    eng = Engine(n_games=64, sims=8)
-    eng.set_precision('f16x3')
-    torch.manual_seed(0)
-    eng.set_weights(Network())
-    pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=6)])
-    eng.set_net_variant(0)
-    l0, v0 = eng.evaluate(pos)
-    eng.set_net_variant(var)
-    l1, v1 = eng.evaluate(pos)
-    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
-    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+    eng = Engine(n_games=4, sims=2)
+    for prec, good, bad in (('f16f8', [0, 8192, 2097152], [16384, 32768, 65536, 131072, 2048, 512]),
+                            ('f16x3', [0, 1024], [512, 4, 8, 2048, 8192])):
+        eng.set_precision(prec)
+        for v in good:
+            eng.set_net_variant(v)
+        for v in bad:
+            with pytest.raises(_lib.MtazError):
+                eng.set_net_variant(v)
 
 
 def test_z_mix_epilogue_bit_identical():

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Network-only microbenchmark and in-process A/B of the fp16x3 network kernels
-(variant 0 = product k_net_y; +512 = k_net_x; low bits = schedules).
+"""Network-only microbenchmark and in-process A/B of the network kernels (PRECISION:VARIANT, e.g.
+f16f8:0 = the product k_net_z, f16x3:0 = k_net_y).  --diag builds and loads libmtaz_diag.so
+(-DMTAZ_NET_DIAG), which also holds the A/B and timing-only variants the product library rejects.
 
 For each variant (interleaved over --rounds, one process, one device; MI355X devices
 clock ~10% apart, so only same-process comparisons mean anything):
@@ -30,8 +31,12 @@ def main():
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--variants', default='0', help='comma list of VARIANT or PRECISION:VARIANT '
                                                    '(e.g. f16x3:0,f16f8:0,f16f8:2048)')
-    ap.add_argument('--precision', default='f16x3')
+    ap.add_argument('--precision', default='f16f8')
+    ap.add_argument('--diag', action='store_true', help='load the diagnostic library (all variants)')
     args = ap.parse_args()
+    if args.diag:
+        from minitchess_alphazero_amd.build import build
+        os.environ['MTAZ_LIB'] = build(verbose=False, diag=True)
     import torch
     from minitchess_alphazero_amd import _lib
     from minitchess_alphazero_amd.engine import Engine, FLOP_PER_EVAL

@@ -15,7 +15,20 @@ from oracle.net import seed0_network
 from oracle.encoder import process_observation
 from tests_positions import random_fens
 torch.set_num_threads(8)
-net = seed0_network().double()
+def _load():
+    # argv[1]: a state_dict (safetensors or torch.save) instead of the seed-0 weights
+    if len(sys.argv) > 1:
+        from oracle.net import Network
+        if sys.argv[1].endswith('.safetensors'):
+            from safetensors.torch import load_file
+            sd = load_file(sys.argv[1])
+        else:
+            sd = torch.load(sys.argv[1], map_location='cpu', weights_only=True)
+        n = Network()
+        n.load_state_dict(sd)
+        return n.eval()
+    return seed0_network()
+net = _load().double()
 fens = random_fens(300, seed=3)
 toks = torch.cat([process_observation(f)[0] for f in fens]); clk = torch.cat([process_observation(f)[1] for f in fens]).double()
 def fold(block):
@@ -43,7 +56,7 @@ def fwd(mode):
         v = net.vlinear(torch.cat([net.vconv(x).view(-1,30), clk],1))
         return p, v
 p0,v0 = fwd('exact')
-net32 = seed0_network()
+net32 = _load()
 with torch.no_grad():
     p32, v32 = net32((toks, clk.float()))
 def report(name, p, v):
