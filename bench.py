@@ -27,6 +27,11 @@ HBM_PEAK_GBS = 8000.0                # MI355X_MICROARCH.md HBM peak
 TREE_BYTES_PER_SIM = 700             # SURVEY 8d algorithmic bytes per simulation of the tree walk
 
 
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f'[bench] {msg}', file=sys.stderr, flush=True)
+
+
 def _cpu_game(job):
     """One seeded game of the oracle's restatement of the app/puppet CPU path (batch-1 torch-CPU
     fp32 per leaf, FEN-keyed dict tables, Python rules) on `threads` torch threads."""
@@ -59,6 +64,7 @@ def cpu_baseline(plan, all_threads, gpu_sims):
             with ctx.Pool(len(seeds) if thr == 1 else 1) as pool:
                 games = pool.map(_cpu_game, [(sims, s, thr) for s in seeds], chunksize=1)
             secs = [g['seconds'] for g in games]
+            log(f'cpu baseline {sims} sims, {thr} thread(s): {[round(x, 1) for x in secs]} s per game')
             runs[f'{sims}sims/{tag}'] = {
                 'threads': thr, 'seeds': seeds, 'seconds_per_game': [round(x, 3) for x in secs],
                 'games_per_s': len(secs) / sum(secs), 'plies': [g['plies'] for g in games],
@@ -189,8 +195,9 @@ def main():
     eng.set_timing(True)
     eng.set_pipeline(args.groups)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         eng.play()
+        log(f'warmup {i + 1}/{args.warmup}')
 
     def sync():
         torch.cuda.synchronize(device)
@@ -201,10 +208,12 @@ def main():
            'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0, 'select_ms': 0.0}
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         st = eng.play()
         for k in tot:
             tot[k] += st[k]
+        if rank == 0:
+            log(f'step {i + 1}/{args.steps}: {st["wall_ms"] / 1e3:.2f} s')
     sync()
     dt = time.perf_counter() - t0
     dt, tot = reduce_run(dt, tot, dist, red_device)
@@ -224,6 +233,8 @@ def main():
         dt2 = time.perf_counter() - t1
         tot2 = {k: st2[k] for k in tot}
         dt2, tot2 = reduce_run(dt2, tot2, dist, red_device)
+        if rank == 0:
+            log(f'secondary (k_net_y) step: {dt2:.2f} s')
         eng.set_precision(args.precision)
         secondary = {'precision': 'f16x3 (fp16 hi/lo split, three f16 MFMA passes; fp32-accurate to ~1e-8)',
                      'value': G * world / dt2, 'unit': 'games/s', 'steps': 1, 'ms_per_step': dt2 * 1e3,

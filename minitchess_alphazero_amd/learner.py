@@ -430,6 +430,7 @@ class LearnPuppet:
     def _init_dataset(self):
         self._dataset = SimpleAlphaZeroDataset(max_length=self._max_length)
         self._records = EpisodeRecords.concat([])
+        self._arrivals = []          # ('rows', list of dicts) / ('records', EpisodeRecords), in push order
         if getattr(self, '_replay', None) is not None:
             self._replay.clear()
 
@@ -465,12 +466,14 @@ class LearnPuppet:
         if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
             self._episode_counter += 1
             self._dataset.push(data)
+            self._arrivals.append(('rows', data))
 
     def push_records(self, records, episodes):
         """push_data for packed rows (EpisodeRecords) of `episodes` episodes.  On a GPU learner
         the rows go straight into the HBM replay ring (ReplayBuffer), encoded on arrival."""
         if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
             self._episode_counter += episodes
+            self._arrivals.append(('records', records))
             if self._learner._device.type == 'cuda':
                 if self._replay is None:
                     self._replay = ReplayBuffer(self._max_length, self._learner._device)
@@ -484,7 +487,14 @@ class LearnPuppet:
         'loss'; encode=False puts the state_dict itself under 'weights' (for callers that move
         the tensors over torch.distributed instead of HTTP, minitchess_alphazero_amd.loop)."""
         self._network.load_state_dict(self.weights)
-        if self._replay is not None and len(self._replay):
+        kinds = {k for k, _ in self._arrivals}
+        if kinds == {'rows', 'records'}:
+            # both push paths were used: train on every row in arrival order, as the reference's
+            # one dataset holds everything pushed since the last update (exp/dataset.py:12-13)
+            data = SimpleAlphaZeroDataset(max_length=self._max_length)
+            for kind, payload in self._arrivals:
+                data.push(payload if kind == 'rows' else payload.to_rows())
+        elif self._replay is not None and len(self._replay):
             data = self._replay
         else:
             data = self._records if len(self._records) else self._dataset

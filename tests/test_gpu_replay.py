@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import REPO, GOLDEN
 
 pytestmark = pytest.mark.gpu
 
@@ -102,8 +102,9 @@ def test_update_from_ring_equals_update_from_records():
     """The ring feeds update() the same batches, in the same order, as the host records.
     With lr=0 the weights never move, so every batch's loss depends only on its rows: the two
     runs must agree to 1e-6 on all 5 batches.  With lr=1e-3 the first loss is bitwise equal and
-    the rest drift only by the GPU backward's non-deterministic reductions (atomics in the
-    conv weight gradients; ~1e-3 relative after 4 AdamW steps), hence rtol=1e-2 there."""
+    the rest drift by the GPU backward's non-deterministic reductions, which drift the host-record
+    path against itself by the same order (test_learner_drift_is_nondeterministic_reduction, which
+    also shows the two paths bitwise equal under deterministic algorithms), hence rtol=1e-2 there."""
     from minitchess_alphazero_amd.learner import ReplayBuffer, SimpleAlphaZeroLearner
     from minitchess_alphazero_amd.network import Network
     rec = _engine_records(16, 8, seed=1)
@@ -124,6 +125,47 @@ def test_update_from_ring_equals_update_from_records():
     a, b = run(rec, 1e-3), run(buf, 1e-3)
     assert len(a) == len(b) == 5
     assert abs(a[0] - b[0]) <= 1e-6 * abs(a[0]) and np.allclose(a, b, rtol=1e-2)
+
+
+def test_learner_drift_is_nondeterministic_reduction(record_property):
+    """Where the lr > 0 drift between the ring and the host records comes from.  (1) The host-record
+    path run twice against itself drifts by the same order (the GPU backward's reductions are not
+    bitwise reproducible).  (2) Under torch.use_deterministic_algorithms(True) with deterministic
+    MIOpen convolutions, two runs of one path are bitwise equal, and the ring equals the host
+    records bitwise: the two paths feed identical batches, and the drift is the reductions'."""
+    from minitchess_alphazero_amd.learner import ReplayBuffer, SimpleAlphaZeroLearner
+    from minitchess_alphazero_amd.network import Network
+    rec = _slice(_engine_records(16, 8, seed=1), 0, 150)
+    buf = ReplayBuffer(1000, 'cuda')
+    buf.push_records(rec)
+
+    def run(data):
+        torch.manual_seed(0)
+        lrn = SimpleAlphaZeroLearner(None, 36, Network(), 32, 1, {'lr': 1e-3}, device='cuda')
+        torch.manual_seed(7)
+        lrn.update(data)
+        return np.array(lrn.last_losses)
+
+    a1, a2 = run(rec), run(rec)
+    self_drift = float(np.max(np.abs(a1 - a2) / np.abs(a1)))
+    prev = (torch.are_deterministic_algorithms_enabled(), torch.backends.cudnn.deterministic,
+            torch.backends.cudnn.benchmark)
+    torch.use_deterministic_algorithms(True)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        d1, d2, d3 = run(rec), run(rec), run(buf)
+    finally:
+        torch.use_deterministic_algorithms(prev[0])
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev[1], prev[2]
+    msg = (f'records vs records, default algorithms: max relative loss drift {self_drift:.3e}; '
+           f'deterministic: {d1.tolist()} / ring {d3.tolist()}')
+    record_property('drift', msg)
+    print(msg)
+    os.makedirs(os.path.join(REPO, 'gpurun_out'), exist_ok=True)
+    with open(os.path.join(REPO, 'gpurun_out', 'learner_drift.txt'), 'w') as fh:
+        fh.write(msg + '\n')
+    assert np.array_equal(d1, d2)
+    assert np.array_equal(d1, d3)
 
 
 def test_learn_puppet_uses_ring():
