@@ -50,26 +50,36 @@ def _cpu_game(job):
 def cpu_baseline(plan, all_threads, gpu_sims):
     """seeded games (np.random.seed(g), random-init weights) at C1's 32 sims and
     at the GPU's sims per move, each on all cores (games one after another, torch.set_num_threads =
-    all_threads) and on 1 thread (the games in parallel, one single-threaded process each: every
-    game still runs on exactly one core).  Children are separate processes (spawned, never
-    exec'ed over this one) and touch no GPU.  value = games/s at the GPU's sims on all cores."""
+    all_threads) and on 1 thread (all single-thread games at once, one process each: every game
+    still runs alone on one core).  Children are separate processes (spawned, never exec'ed over
+    this one) and touch no GPU.  value = games/s at the GPU's sims on all cores."""
     import multiprocessing as mp
     seeds = [0, 1, 2] if plan == 'full' else [0]
     sims_list = sorted({32, gpu_sims}) if plan == 'full' else [gpu_sims]
     ctx = mp.get_context('spawn')
     runs = {}
+
+    def record(sims, thr, games):
+        secs = [g['seconds'] for g in games]
+        log(f'cpu baseline {sims} sims, {thr} thread(s): {[round(x, 1) for x in secs]} s per game')
+        runs[f'{sims}sims/{"all" if thr == all_threads else thr}'] = {
+            'threads': thr, 'seeds': seeds, 'seconds_per_game': [round(x, 3) for x in secs],
+            'games_per_s': len(secs) / sum(secs), 'plies': [g['plies'] for g in games],
+            'nn_evals': [g['nn_evals'] for g in games],
+            'sims_per_s': sum(g['plies'] for g in games) * sims / sum(secs)}
+
+    if plan == 'full':
+        # 1 thread: every (sims, seed) game at once, one single-threaded process each (6 of the
+        # host's cores, each game alone on its core)
+        jobs = [(sims, sd, 1) for sims in sims_list for sd in seeds]
+        with ctx.Pool(len(jobs)) as pool:
+            out = pool.map(_cpu_game, jobs, chunksize=1)
+        for i, sims in enumerate(sims_list):
+            record(sims, 1, out[i * len(seeds):(i + 1) * len(seeds)])
+    # all cores: the games one after another in one process
     for sims in sims_list:
-        modes = [('all', all_threads)] + ([('1', 1)] if plan == 'full' else [])
-        for tag, thr in modes:
-            with ctx.Pool(len(seeds) if thr == 1 else 1) as pool:
-                games = pool.map(_cpu_game, [(sims, s, thr) for s in seeds], chunksize=1)
-            secs = [g['seconds'] for g in games]
-            log(f'cpu baseline {sims} sims, {thr} thread(s): {[round(x, 1) for x in secs]} s per game')
-            runs[f'{sims}sims/{tag}'] = {
-                'threads': thr, 'seeds': seeds, 'seconds_per_game': [round(x, 3) for x in secs],
-                'games_per_s': len(secs) / sum(secs), 'plies': [g['plies'] for g in games],
-                'nn_evals': [g['nn_evals'] for g in games],
-                'sims_per_s': sum(g['plies'] for g in games) * sims / sum(secs)}
+        with ctx.Pool(1) as pool:
+            record(sims, all_threads, pool.map(_cpu_game, [(sims, sd, all_threads) for sd in seeds], chunksize=1))
     head = runs[f'{gpu_sims}sims/all']
     return {'value': head['games_per_s'], 'unit': 'games/s', 'cores': all_threads, 'kind': 'port',
             'sample': (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
@@ -119,6 +129,7 @@ def main():
     ap.add_argument('--sims', type=int, default=64, help='MCTS simulations per move (config 2: 64)')
     ap.add_argument('--precision', default='f16f8', choices=['f16x3', 'f16f8', 'fp32'])
     ap.add_argument('--groups', type=int, default=1, help='game groups on separate HIP streams (mtaz_set_pipeline)')
+    ap.add_argument('--net-variant', type=int, default=0, help='parity-tested network build (Engine.set_net_variant)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--cpu-plan', default='full', choices=['full', 'quick'],
@@ -192,6 +203,7 @@ def main():
         torch.manual_seed(0)                      # random-init weights of the reference architecture
         eng.set_weights(Network())
     eng.set_precision(args.precision)
+    eng.set_net_variant(args.net_variant)
     eng.set_timing(True)
     eng.set_pipeline(args.groups)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing

@@ -142,11 +142,6 @@ struct NetWeights {
   // Value q of the vector (bits 6q..6q+5) is channel perm(q) = 16*((q>>2)&1) + 4*(q>>3) + (q&3)
   // of the 32-channel block: the order in which the epilogue's lanes hold them.
   const uint4* conv6;
-  // k_net_z VAR 262144 (ds_read_b64 operand reads): convy and conv8 with the two 8-byte halves of
-  // every 16 B swapped in the lanes of odd K group (l>>4): those lanes read their LDS fragments
-  // half-swapped, which keeps each 32-lane read group on distinct banks
-  const uint4* convz;
-  const uint4* conv8z;
 };
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304

@@ -997,26 +997,15 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.yrange = h->wyrange;
   const size_t nx = wy.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
   const size_t nsc = (sc8.size() + 3) / 4, n6 = w6.size() / 16;
-  // half-swapped copies for the ds_read_b64 build (NetWeights::convz, conv8z)
-  std::vector<_Float16> wz(wy);
-  for (size_t u = 0; u < wz.size() / 8; ++u)
-    if (((u % 64) >> 4) & 1)
-      for (int j = 0; j < 4; ++j) std::swap(wz[u * 8 + j], wz[u * 8 + 4 + j]);
-  std::vector<uint8_t> w8z(w8);
-  for (size_t u = 0; u < w8z.size() / 16; ++u)
-    if (((u % 64) >> 4) & 1)
-      for (int j = 0; j < 8; ++j) std::swap(w8z[u * 16 + j], w8z[u * 16 + 8 + j]);
-  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6 | convz | conv8z
-  const size_t o_sy = nx, o_w8 = o_sy + nsy, o_sc = o_w8 + n8, o_w6 = o_sc + nsc, o_z = o_w6 + n6;
-  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, o_z + nx + n8));
+  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6
+  const size_t o_sy = nx, o_w8 = o_sy + nsy, o_sc = o_w8 + n8, o_w6 = o_sc + nsc, o_end = o_w6 + n6;
+  if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, o_end));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
   HIPCHK(hipMemcpy(h->wxbuf, wy.data(), nx * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_sy, sy.data(), nsy * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_w8, w8.data(), n8 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_sc, sc8.data(), sc8.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_w6, w6.data(), n6 * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + o_z, wz.data(), nx * 16, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(h->wxbuf + o_z + nx, w8z.data(), n8 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx_inv = h->wxinv;
   h->w.stemx_inv = h->wxinv + CONV_LAYERS;
@@ -1025,8 +1014,6 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.conv8 = h->wxbuf + o_w8;
   h->w.conv8_sc = reinterpret_cast<const int32_t*>(h->wxbuf + o_sc);
   h->w.conv6 = h->wxbuf + o_w6;
-  h->w.convz = h->wxbuf + o_z;
-  h->w.conv8z = h->wxbuf + o_z + nx;
   h->weights_ok = true;
   return 0;
 }
@@ -1096,7 +1083,8 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
   if (h->precision == NET_F16X3) ok = ok || variant == 1024;
-  if (h->precision == NET_F16F8) ok = ok || variant == 2097152 || variant == 8192;
+  if (h->precision == NET_F16F8)
+    ok = ok || variant == 2097152 || variant == 8192;
 #ifdef MTAZ_NET_DIAG
   ok = true;
 #endif

@@ -25,10 +25,7 @@
 // weight groups GD groups ahead (half a group per step), this step's e4m3 activation
 // fragments during phase A and the next step's f16 ones during phase B.
 //
-// Waves: 8 (2 per SIMD), 32 output channels each.  VAR 2048 = 4 waves of 64 channels, k_net_y's
-// layout; there the operands do not fit the 256 arch VGPRs beside the address arithmetic (the
-// compiler parks some in AGPRs and shuffles them), with 8 waves each wave's weights halve and
-// the accumulators take 64 AGPRs.  VAR 4096: prefetch one step / one e4m3 group further ahead.
+// Waves: 8 (2 per SIMD), 16 accumulator tiles each; the wave layouts are described at ZCfg.
 #include "net_common.h"
 
 namespace mtaz {
@@ -42,13 +39,6 @@ constexpr int GZ = 36;       // e4m3 groups per conv
 __device__ __forceinline__ i32x8 cat8(uint4 a, uint4 b) {
   return (i32x8){(int)a.x, (int)a.y, (int)a.z, (int)a.w, (int)b.x, (int)b.y, (int)b.z, (int)b.w};
 }
-
-// 16 B at p as two 8-B reads, the half at byte h (0 or 8) first
-__device__ __forceinline__ uint4 rd8x2(const char* p, int h) {
-  const uint2 a = *reinterpret_cast<const uint2*>(p + h), b = *reinterpret_cast<const uint2*>(p + (h ^ 8));
-  return make_uint4(a.x, a.y, b.x, b.y);
-}
-__device__ __forceinline__ f16x8 rd16x2(const char* p, int h) { return __builtin_bit_cast(f16x8, rd8x2(p, h)); }
 
 // f32(half of pk) * b + c in one v_fma_mix_f32 (the compiler does not form it with f32
 // denormals on).  Bit-identical to the unfused form (round the product, then add) where the
@@ -74,16 +64,38 @@ __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d)
   return (uint32_t)r;
 }
 
+// Wave layout.  VAR 0: 8 waves, wave w owns output channels [32w, 32w + 32) (CT = 2 channel tiles)
+// on all 4 boards.  Diagnostic library only: VAR 4194304 (board pairs), 8 waves as 4 channel
+// groups x 2 board pairs, wave w owning channels [64(w&3), +64) (CT = 4) on boards 2(w>>2) and
+// 2(w>>2) + 1: the same 16 accumulator tiles per wave with half the LDS bytes per MFMA and twice
+// the weight loads; bit-identical results, 3% more cycles at a 5% lower clock.
+// VAR 2048: 4 waves of 64 channels on all 4 boards.
 template <int VAR>
-constexpr int zWaves = (VAR & 2048) ? 4 : 8;
+struct ZCfg {
+  static constexpr bool BP = (VAR & 4194304) != 0;
+  static constexpr int NW = (VAR & 2048) ? 4 : 8;   // waves
+  static constexpr int BPW = BP ? 2 : XB;           // boards per wave
+  static constexpr int CT = BP ? 4 : 16 / NW;       // channel tiles (of 16) per wave
+  static constexpr int NCG = 16 / CT;               // channel groups
+  static constexpr int TW = 2 * BPW;                // column tiles (board x square tile) per wave
+  static_assert(NCG * (XB / BPW) == NW, "waves cover channel groups x board groups");
+};
+
+// element bb of a 4-board register array with a wave-uniform runtime index, without a
+// dynamically indexed local array (which would live in scratch)
+template <class T>
+__device__ __forceinline__ T pick4(const T* a, int bb) {
+  return bb == 0 ? a[0] : bb == 1 ? a[1] : bb == 2 ? a[2] : a[3];
+}
 
 template <bool STAMP, int VAR>
-__global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights W, const Pos* __restrict__ pos,
-                                                               const int32_t* __restrict__ count, int max_b, int mode,
-                                                               float* __restrict__ logits_out,
-                                                               float* __restrict__ values_out,
-                                                               unsigned long long* __restrict__ stamps) {
-  constexpr int NW = zWaves<VAR>, NT = 64 * NW, CT = 16 / NW;   // waves, threads, channel tiles per wave
+__global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeights W, const Pos* __restrict__ pos,
+                                                                 const int32_t* __restrict__ count, int max_b,
+                                                                 int mode, float* __restrict__ logits_out,
+                                                                 float* __restrict__ values_out,
+                                                                 unsigned long long* __restrict__ stamps) {
+  using C = ZCfg<VAR>;
+  constexpr int NW = C::NW, NT = 64 * NW, CT = C::CT, BPW = C::BPW, TW = C::TW;
   constexpr bool F6 = (VAR & 8192) != 0;   // cross terms in e2m3 blocks (epilogue6, NetWeights::conv6)
   // diagnostic builds (timing only, wrong results): 16384 = every layer reads layer 0's weights
   // (an L2-resident weight set), 32768 = every step reads k-block / group 0 (L1-resident)
@@ -91,12 +103,6 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   // 65536 = no cross-term MFMAs (phase B issues its loads only), 131072 = no activation LDS reads
   // in the K loop (the fragments of step 0 are reused)
   constexpr bool DIAG_NOB = (VAR & 65536) != 0, DIAG_NOLDS = (VAR & 131072) != 0;
-  // 262144: activation fragments by ds_read_b64 pairs, the lanes of odd K group reading each 16 B
-  // upper half first (weights: NetWeights::convz / conv8z; e2m3 blocks: stored half-swapped by the
-  // odd waves), so that the 32 lanes of a read group cover every bank once (4.9 LDS cycles per
-  // 16 B on the K loop's access pattern vs 7.2 for ds_read_b128, tools/lds_conflicts.py)
-  constexpr bool R64 = (VAR & 262144) != 0;
-  constexpr bool TBL = (VAR & 524288) != 0;   // per-row swizzle table (net_common.h hz)
   // 1048576: static issue priority 1 for the second-dispatched half of the waves (the arbitration
   // loser of each SIMD pair, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
   constexpr bool PRIO = (VAR & 1048576) != 0;
@@ -109,6 +115,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   if (b0 >= nb) return;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, n = lane & 15, g = lane >> 4;
+  const int wc = wave % C::NCG, wb0 = BPW * (wave / C::NCG);   // channel group, first board
   unsigned long long t_prev = 0, st_stem = 0, st_k = 0, st_epi = 0, st_heads = 0;
   unsigned long long t_start = 0, r_start = 0;
   if constexpr (STAMP) {
@@ -125,9 +132,10 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 
   const int p1 = 16 + n;
   const int ph0 = n / 5, pw0 = n % 5, ph1 = p1 / 5, pw1 = p1 % 5;
-  f32x4v acc[CT * 8];
+  // accumulator tile ct * TW + 2 j + pt: channel tile ct, board wb0 + j, square tile pt
+  f32x4v acc[CT * TW];
 #pragma unroll
-  for (int i = 0; i < CT * 8; ++i) acc[i] = (f32x4v){0};
+  for (int i = 0; i < CT * TW; ++i) acc[i] = (f32x4v){0};
   int overflow = 0;
 
   // dynamic range (k_net_y): the image holds x * 2^-xs, one xs per workgroup (0 for any ordinary
@@ -143,6 +151,31 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   // Xl8 = e4m3(Xl * 2^(sh[bb] + 11)).  Per board (from the board's own bound), so a board's
   // results do not depend on the boards it shares a workgroup with.
   int sh[XB] = {0, 0, 0, 0};
+
+  // per-board maxima of the wave's new outputs -> the workgroup's per-board maxima (mxb) after the
+  // epilogue's barrier; y >= 0, so float bits order as values
+  auto publish_max = [&](float* ymax, int xo) {
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) ymax[j] = fmaxf(ymax[j], __shfl_xor(ymax[j], o, 64));
+    }
+    if (lane < BPW) {
+      float m = ymax[0];
+#pragma unroll
+      for (int j = 1; j < BPW; ++j) m = lane == j ? ymax[j] : m;
+      atomicMax(&mxs[slot * XB + wb0 + lane], __float_as_uint(m));
+    }
+    if (tid < XB) mxs[(slot ^ 1) * XB + tid] = 0u;   // every wave read them before this epilogue's barrier
+    xs = xo;
+    __syncthreads();
+#pragma unroll
+    for (int bb = 0; bb < XB; ++bb) {
+      mxb[bb] = __builtin_ldexpf(__uint_as_float(mxs[slot * XB + bb]), xo);
+      if (!__builtin_isfinite(mxb[bb])) overflow = 1;
+    }
+    slot ^= 1;
+  };
 
   // Epilogue: y = ReLU(acc * 2^(xs - e - xo) + bias * 2^-xo) in stored units; part 0 <- f16(y),
   // part 1 <- e4m3 copies of y - f16(y) and f16(y).  Conv A seeds conv B's accumulators with the
@@ -164,79 +197,85 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     // board bb's stored values are <= boundb[bb] * 2^-xo =: bs; sh_new = 7 - ilogb(bs) keeps
     // e4m3(Xh * 2^sh) < 256 (clamped so that 2^(sh + 11) stays a normal float)
     int sh_new[XB];
-    float hs[XB], ls[XB], ls_in[XB];
+    float hs[BPW], ls[BPW], ls_in[BPW];
 #pragma unroll
     for (int bb = 0; bb < XB; ++bb) {
       const float bs = __builtin_ldexpf(boundb[bb], -xo);
       const int eb = bs > 0.f ? (int)((__float_as_uint(bs) >> 23) & 0xffu) - 127 : -126;
       int e = bs < __builtin_inff() ? 7 - eb : 0;
       sh_new[bb] = e > 60 ? 60 : e < -60 ? -60 : e;
-      hs[bb] = __builtin_ldexpf(1.f, sh_new[bb]);
-      ls[bb] = __builtin_ldexpf(1.f, sh_new[bb] + 11);
-      ls_in[bb] = __builtin_ldexpf(sseed, -(sh[bb] + 11));   // Xl8 units of the image being read
     }
-    float ymax[XB] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+      const int snew = pick4(sh_new, wb0 + j), sold = pick4(sh, wb0 + j);
+      hs[j] = __builtin_ldexpf(1.f, snew);
+      ls[j] = __builtin_ldexpf(1.f, snew + 11);
+      ls_in[j] = __builtin_ldexpf(sseed, -(sold + 11));   // Xl8 units of the image being read
+    }
+    float ymax[BPW];
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) ymax[j] = 0.f;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const int co0 = 16 * CT * wave + 16 * ct + 4 * g;
+      const int co0 = 16 * CT * wc + 16 * ct + 4 * g;
       const float4 bu = *reinterpret_cast<const float4*>(bias + co0);
       const float4 bv = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int bb = t >> 1, pt = t & 1;
-        f32x4v& a = acc[ct * 8 + t];
+      for (int t = 0; t < TW; ++t) {
+        const int j = t >> 1, bb = wb0 + j, pt = t & 1;
+        f32x4v& a = acc[ct * TW + t];
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
-          const int ah = ioffs<TBL>(0, bb, p, co0 >> 3) + 8 * (g & 1);
-          const int al8 = ioffs<TBL>(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
-          const int ah8 = ioffs<TBL>(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
+          const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1);
+          const int al8 = ioff(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
+          const int ah8 = ioff(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
           float y[4];
           y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
           y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
           y[2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv.z), 0.f);
           y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
-          ymax[bb] = fmaxf(fmaxf(ymax[bb], fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
+          ymax[j] = fmaxf(fmaxf(ymax[j], fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
           if constexpr (conv_a) {
             const int xl = *reinterpret_cast<const int*>(smem + al8);
             if constexpr (NOMIX) {
               const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
-              a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[bb]);
-              a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[bb]);
-              a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[bb]);
-              a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[bb]);
+              a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[j]);
+              a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[j]);
+              a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[j]);
+              a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[j]);
             } else {
               const uint2 xp = *reinterpret_cast<const uint2*>(smem + ah);
-              a[0] = zmix_lo(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[bb]);
-              a[1] = zmix_hi(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[bb]);
-              a[2] = zmix_lo(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[bb]);
-              a[3] = zmix_hi(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[bb]);
+              a[0] = zmix_lo(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[j]);
+              a[1] = zmix_hi(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[j]);
+              a[2] = zmix_lo(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[j]);
+              a[3] = zmix_hi(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[j]);
             }
           } else {
             a = (f32x4v){0};
           }
           f16x4 yh;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
+          for (int q = 0; q < 4; ++q) yh[q] = (_Float16)y[q];
           float h[4], l[4];
           if constexpr (NOMIX) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              h[j] = (float)yh[j];
-              l[j] = (y[j] - h[j]) * ls[bb];   // exact difference, power-of-two scale
-              h[j] *= hs[bb];
+            for (int q = 0; q < 4; ++q) {
+              h[q] = (float)yh[q];
+              l[q] = (y[q] - h[q]) * ls[j];   // exact difference, power-of-two scale
+              h[q] *= hs[j];
             }
           } else {
             // l = y ls - h ls (= (y - h) ls, exact) and h hs straight from the packed halves
             const uint2 yp = __builtin_bit_cast(uint2, yh);
-            const float nl = -ls[bb];
-            l[0] = zmix_lo(yp.x, nl, y[0] * ls[bb]);
-            l[1] = zmix_hi(yp.x, nl, y[1] * ls[bb]);
-            l[2] = zmix_lo(yp.y, nl, y[2] * ls[bb]);
-            l[3] = zmix_hi(yp.y, nl, y[3] * ls[bb]);
-            h[0] = zmix_lo(yp.x, hs[bb], 0.f);
-            h[1] = zmix_hi(yp.x, hs[bb], 0.f);
-            h[2] = zmix_lo(yp.y, hs[bb], 0.f);
-            h[3] = zmix_hi(yp.y, hs[bb], 0.f);
+            const float nl = -ls[j];
+            l[0] = zmix_lo(yp.x, nl, y[0] * ls[j]);
+            l[1] = zmix_hi(yp.x, nl, y[1] * ls[j]);
+            l[2] = zmix_lo(yp.y, nl, y[2] * ls[j]);
+            l[3] = zmix_hi(yp.y, nl, y[3] * ls[j]);
+            h[0] = zmix_lo(yp.x, hs[j], 0.f);
+            h[1] = zmix_hi(yp.x, hs[j], 0.f);
+            h[2] = zmix_lo(yp.y, hs[j], 0.f);
+            h[3] = zmix_hi(yp.y, hs[j], 0.f);
           }
           *reinterpret_cast<f16x4*>(smem + ah) = yh;
           *reinterpret_cast<uint32_t*>(smem + al8) = pk_fp8x4(l[0], l[1], l[2], l[3]);
@@ -246,37 +285,20 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         }
       }
     }
-    // per-board maxima of the new image (y >= 0: float bits order as values)
-#pragma unroll
-    for (int bb = 0; bb < XB; ++bb) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) ymax[bb] = fmaxf(ymax[bb], __shfl_xor(ymax[bb], o, 64));
-    }
-    if (lane < XB) {
-      const float m = lane == 0 ? ymax[0] : lane == 1 ? ymax[1] : lane == 2 ? ymax[2] : ymax[3];
-      atomicMax(&mxs[slot * XB + lane], __float_as_uint(m));
-    }
-    if (tid < XB) mxs[(slot ^ 1) * XB + tid] = 0u;   // every wave read them before this epilogue's barrier
-    xs = xo;
 #pragma unroll
     for (int bb = 0; bb < XB; ++bb) sh[bb] = sh_new[bb];
-    __syncthreads();
-#pragma unroll
-    for (int bb = 0; bb < XB; ++bb) {
-      mxb[bb] = __builtin_ldexpf(__uint_as_float(mxs[slot * XB + bb]), xo);
-      if (!__builtin_isfinite(mxb[bb])) overflow = 1;
-    }
-    slot ^= 1;
+    publish_max(ymax, xo);
   };
 
-  // VAR 8192 epilogue: the cross-term copies in e2m3 (fp6) blocks instead of e4m3 bytes.  Wave w
-  // owns the 32 output channels of block w (= K block 4c + g of the next conv's 128-channel chunk
-  // c), and per square its lane g holds channels 16 ct + 4 g + i (ct, i < 4): values 8 g + 4 ct + i
-  // of the block's 32-value fp6 vector (NetWeights::conv6 packs the weights in that order), bits
-  // 48 g .. 48 g + 47 = bytes 6 g .. 6 g + 5 of the 32-B block slot (term 0: Xl, chunks 2 w, 2 w + 1
-  // of part 1; term 1: Xh, chunks 16 + 2 w, 17 + 2 w), its e8m0 scale at byte 24.  The scale
-  // covers the block's largest |value| (a rounded-up 16-bit key, max over the 4 lanes g), so that
-  // every value is <= 7.5 in scaled units; codes by e4m3 RNE of v * 2^(-s-6) (fp6_scale_probe).
+  // VAR 8192 epilogue: the cross-term copies in e2m3 (fp6) blocks instead of e4m3 bytes.  The
+  // wave's channel tiles pair up into 32-channel blocks blk = (CT/2) wc + bi (= K block 4c + g of
+  // the next conv's 128-channel chunk c), and per square its lane g holds channels 16 ct + 4 g + i
+  // (ct, i < 4) of the block: values 8 g + 4 ct + i of the block's 32-value fp6 vector
+  // (NetWeights::conv6 packs the weights in that order), bits 48 g .. 48 g + 47 = bytes 6 g .. 6 g + 5
+  // of the 32-B block slot (term 0: Xl, chunks 2 blk, 2 blk + 1 of part 1; term 1: Xh, chunks
+  // 16 + 2 blk, 17 + 2 blk), its e8m0 scale at byte 24.  The scale covers the block's largest
+  // |value| (a rounded-up 16-bit key, max over the 4 lanes g), so that every value is <= 7.5 in
+  // scaled units; codes by e4m3 RNE of v * 2^(-s-6) (fp6_scale_probe).
   auto epilogue6 = [&](float inv, const float* bias, auto conv_a_t, float s_next, const float* boundb) {
     constexpr bool conv_a = decltype(conv_a_t)::value;
     int el = lane;
@@ -286,13 +308,13 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     const int xo = bound >= 16384.f ? (int)((__float_as_uint(bound) >> 23) & 0xffu) - 127 - 14 : 0;
     const float in_scale = __builtin_ldexpf(inv, xs - xo), st = __builtin_ldexpf(1.f, -xo);
     const float sseed = __builtin_ldexpf(s_next, xs - xo);
-    float ymax[XB] = {0.f, 0.f, 0.f, 0.f};
-    // wave w owns blocks (CT/2) w .. (CT/2) w + CT/2 - 1 (one with 8 waves, two with 4)
+    float ymax[BPW];
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) ymax[j] = 0.f;
 #pragma unroll
     for (int bi = 0; bi < CT / 2; ++bi) {
-      const int blk = (CT / 2) * wave + bi;
-      const int bx = R64 ? 8 * (blk & 1) : 0;   // half-swapped block slots (odd blocks, R64)
-      const int o32 = ((g & 1) ? 6 * g + 2 : 6 * g) ^ bx, o16 = ((g & 1) ? 6 * g : 6 * g + 4) ^ bx, osc = 24 ^ bx;
+      const int blk = (CT / 2) * wc + bi;
+      const int o32 = (g & 1) ? 6 * g + 2 : 6 * g, o16 = (g & 1) ? 6 * g : 6 * g + 4, osc = 24;
       float4 bv[2];
   #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
@@ -300,18 +322,16 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         bv[ct] = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
       }
       // byte address of byte `b` of block blk's slot of term `term` on row p of board bb
-      auto baddr = [&](int term, int bb, int p, int b) {
-        return ioffs<TBL>(1, bb, p, 16 * term + 2 * blk + (b >> 4)) + (b & 15);
-      };
+      auto baddr = [&](int term, int bb, int p, int b) { return ioff(1, bb, p, 16 * term + 2 * blk + (b >> 4)) + (b & 15); };
   #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int bb = t >> 1, pt = t & 1;
+      for (int t = 0; t < TW; ++t) {
+        const int j = t >> 1, bb = wb0 + j, pt = t & 1;
         const bool valid = pt == 0 || p1 < 30;
         const int p = pt ? (valid ? p1 : ZROW) : n;
         float y[8];
   #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
-          const f32x4v& a = acc[(2 * bi + ct) * 8 + t];
+          const f32x4v& a = acc[(2 * bi + ct) * TW + t];
           y[4 * ct + 0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv[ct].x), 0.f);
           y[4 * ct + 1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv[ct].y), 0.f);
           y[4 * ct + 2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv[ct].z), 0.f);
@@ -322,7 +342,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
           for (int k = 0; k < 8; ++k) y[k] = 0.f;
         }
   #pragma unroll
-        for (int k = 0; k < 8; ++k) ymax[bb] = fmaxf(ymax[bb], y[k]);
+        for (int k = 0; k < 8; ++k) ymax[j] = fmaxf(ymax[j], y[k]);
         if constexpr (conv_a) {
           // seed conv B with the block input Xh + Xl (conv B's units)
           float xin[8];
@@ -338,7 +358,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
               const uint32_t c = ct ? B24 : A24;
               uint32_t e = (c & 0x3fu) | ((c << 2) & 0x3f00u) | ((c << 4) & 0x3f0000u) | ((c << 6) & 0x3f000000u);
               e = (e & 0x1f1f1f1fu) | ((e & 0x20202020u) << 2);
-              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1));
+              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ioff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1));
               xin[4 * ct + 0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 0) * lsc);
               xin[4 * ct + 1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 1) * lsc);
               xin[4 * ct + 2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 2) * lsc);
@@ -349,10 +369,11 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
             for (int k = 0; k < 8; ++k) xin[k] = 0.f;
           }
   #pragma unroll
-          for (int ct = 0; ct < 2; ++ct) acc[(2 * bi + ct) * 8 + t] = (f32x4v){xin[4 * ct], xin[4 * ct + 1], xin[4 * ct + 2], xin[4 * ct + 3]};
+          for (int ct = 0; ct < 2; ++ct)
+            acc[(2 * bi + ct) * TW + t] = (f32x4v){xin[4 * ct], xin[4 * ct + 1], xin[4 * ct + 2], xin[4 * ct + 3]};
         } else {
   #pragma unroll
-          for (int ct = 0; ct < 2; ++ct) acc[(2 * bi + ct) * 8 + t] = (f32x4v){0};
+          for (int ct = 0; ct < 2; ++ct) acc[(2 * bi + ct) * TW + t] = (f32x4v){0};
         }
         // hi / lo split, block keys: bf16 bits rounded up (>= the value) of max h, max |l|
         float h[8], l[8], mh = 0.f, ml = 0.f;
@@ -379,7 +400,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         if (valid) {
   #pragma unroll
           for (int ct = 0; ct < 2; ++ct)
-            *reinterpret_cast<f16x4*>(smem + ioffs<TBL>(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
+            *reinterpret_cast<f16x4*>(smem + ioff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
         }
   #pragma unroll
         for (int term = 0; term < 2; ++term) {
@@ -406,24 +427,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
         }
       }
     }
-#pragma unroll
-    for (int bb = 0; bb < XB; ++bb) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) ymax[bb] = fmaxf(ymax[bb], __shfl_xor(ymax[bb], o, 64));
-    }
-    if (lane < XB) {
-      const float m = lane == 0 ? ymax[0] : lane == 1 ? ymax[1] : lane == 2 ? ymax[2] : ymax[3];
-      atomicMax(&mxs[slot * XB + lane], __float_as_uint(m));
-    }
-    if (tid < XB) mxs[(slot ^ 1) * XB + tid] = 0u;
-    xs = xo;
-    __syncthreads();
-#pragma unroll
-    for (int bb = 0; bb < XB; ++bb) {
-      mxb[bb] = __builtin_ldexpf(__uint_as_float(mxs[slot * XB + bb]), xo);
-      if (!__builtin_isfinite(mxb[bb])) overflow = 1;
-    }
-    slot ^= 1;
+    publish_max(ymax, xo);
   };
 
   // ---------------- stem: conv3x3 8->256 in f16x3 (k_net_y's), K = 3 k-blocks -------------
@@ -432,9 +436,9 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   stem_input<NT>(smem, simg, pos, b0, nb, W, tid);
   __syncthreads();
   {
-    const uint4* Ws = W.stemy + (size_t)(CT * wave) * 3 * 128 + lane;
+    const uint4* Ws = W.stemy + (size_t)(CT * wc) * 3 * 128 + lane;
     for (int kb = 0; kb < 3; ++kb) {
-      f16x8 SA[2 * CT], SB[16];
+      f16x8 SA[2 * CT], SB[2 * TW];
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
         SA[2 * c] = __builtin_bit_cast(f16x8, Ws[c * 3 * 128 + kb * 128]);
@@ -446,9 +450,10 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #pragma unroll
       for (int part = 0; part < 2; ++part)
 #pragma unroll
-        for (int bb = 0; bb < XB; ++bb) {
-          SB[part * 8 + 2 * bb] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r0) * 16);
-          SB[part * 8 + 2 * bb + 1] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r1) * 16);
+        for (int j = 0; j < BPW; ++j) {
+          const int bb = wb0 + j;
+          SB[part * TW + 2 * j] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r0) * 16);
+          SB[part * TW + 2 * j + 1] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r1) * 16);
         }
 #pragma unroll
       for (int ps = 0; ps < 3; ++ps) {
@@ -456,8 +461,8 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-          for (int t = 0; t < 8; ++t)
-            acc[ct * 8 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(SA[2 * ct + wp], SB[xp * 8 + t], acc[ct * 8 + t], 0, 0, 0);
+          for (int t = 0; t < TW; ++t)
+            acc[ct * TW + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(SA[2 * ct + wp], SB[xp * TW + t], acc[ct * TW + t], 0, 0, 0);
       }
     }
   }
@@ -477,17 +482,17 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
   if constexpr (PRIO) {
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
-  constexpr bool DEEP = (VAR & 4096) != 0;
-  constexpr int PD = (NW == 8 ? 1 : 2) + (DEEP ? 1 : 0), RA = PD + 1, GD = DEEP ? 2 : 1, RG = GD + 1;
+  constexpr int PD = NW == 8 ? 1 : 2, RA = PD + 1, GD = 1, RG = GD + 1;
   constexpr int U = (RA == 2 && RG == 2) ? 4 : 12;
   static_assert(KBZ % U == 0 && U % RA == 0 && (U / 2) % RG == 0 && RG > GD, "rings");
-  f16x8 A16[RA][CT], B16[8];
-  i32x8 A8[RG][CT], B8[4];
+  f16x8 A16[RA][CT], B16[TW];
+  i32x8 A8[RG][CT], B8[BPW];
   const int n_ = n, p1_ = p1, ph0_ = ph0, pw0_ = pw0, ph1_ = ph1, pw1_ = pw1, g_ = g;
-  const uint4* Wh = (R64 ? W.convz : W.convy) + (size_t)(CT * wave) * KBZ * 128 + lane;   // hi parts
-  const uint4* W8 = (R64 ? W.conv8z : W.conv8) + (size_t)(CT * wave) * GZ * 128 + lane;
-  const uint4* W6 = W.conv6 + (size_t)(CT * wave) * GZ * 112;
+  const uint4* Wh = W.convy + (size_t)(CT * wc) * KBZ * 128 + lane;   // hi parts
+  const uint4* W8 = W.conv8 + (size_t)(CT * wc) * GZ * 128 + lane;
+  const uint4* W6 = W.conv6 + (size_t)(CT * wc) * GZ * 112;
   const int32_t* sc8 = W.conv8_sc;
+  const int bofs = wb0 * IROWS * RB;   // the wave's first board in each image part
 
   // Wh fragments of step (k-block) KB, the wave's channel tiles
 #define Z_LOAD_A16(S, KB)                                                             \
@@ -515,24 +520,18 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
       }                                                                               \
     }                                                                                 \
   }
-  // Xh (f16) fragments of step KB for both square tiles: S16[2 * board + tile]
+  // Xh (f16) fragments of step KB for both square tiles of the wave's boards: S16[2 j + tile]
 #define Z_LOAD_B16(S16, KB)                                                           \
   {                                                                                   \
     const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
     const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
     const int r0_ = src_row(n, ph0, pw0, tap_), r1_ = src_row(p1, ph1, pw1, tap_);    \
-    const int o0_ = r0_ * RB + ((ch_ ^ swz<TBL>(r0_)) << 4);                          \
-    const int o1_ = r1_ * RB + ((ch_ ^ swz<TBL>(r1_)) << 4);                          \
-    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
-      const char* base_ = smem + bb_ * IROWS * RB;                                    \
-      if constexpr (R64) {                                                            \
-        const int h_ = 8 * (g & 1);                                                   \
-        S16[2 * bb_] = rd16x2(smem + bofs[bb_] + o0_, h_);                            \
-        S16[2 * bb_ + 1] = rd16x2(smem + bofs[bb_] + o1_, h_);                        \
-      } else {                                                                        \
-        S16[2 * bb_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                 \
-        S16[2 * bb_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);             \
-      }                                                                               \
+    const int o0_ = r0_ * RB + ((ch_ ^ (r0_ & 15)) << 4);                             \
+    const int o1_ = r1_ * RB + ((ch_ ^ (r1_ & 15)) << 4);                             \
+    _Pragma("unroll") for (int j_ = 0; j_ < BPW; ++j_) {                              \
+      const char* base_ = smem + bofs + j_ * IROWS * RB;                              \
+      S16[2 * j_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                     \
+      S16[2 * j_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);                 \
     }                                                                                 \
   }
   // e4m3 fragments of step KB's group on square tile KB & 1 (Xl8 for term 0, Xh8 for term 1):
@@ -544,17 +543,11 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     const int r_ = (kk_ & 1) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_); \
     const int q0_ = 16 * term_ + 8 * cc_ + 2 * g;                                     \
     /* part-1 row base once, so that the boards' offsets (< 64 KB) fit the ds_read immediate */ \
-    const char* p0_ = smem + PARTB + r_ * RB + ((q0_ ^ swz<TBL>(r_)) << 4);           \
-    const char* p1_ = smem + PARTB + r_ * RB + (((q0_ + 1) ^ swz<TBL>(r_)) << 4);     \
-    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_) {                            \
-      if constexpr (R64) {                                                            \
-        const int h_ = 8 * (g & 1);                                                   \
-        S8[bb_] = cat8(rd8x2(p0_ + bofs[bb_], h_), rd8x2(p1_ + bofs[bb_], h_));       \
-      } else {                                                                        \
-        S8[bb_] = cat8(*reinterpret_cast<const uint4*>(p0_ + bb_ * IROWS * RB),      \
-                       *reinterpret_cast<const uint4*>(p1_ + bb_ * IROWS * RB));     \
-      }                                                                               \
-    }                                                                                 \
+    const char* p0_ = smem + PARTB + bofs + r_ * RB + ((q0_ ^ (r_ & 15)) << 4);        \
+    const char* p1_ = smem + PARTB + bofs + r_ * RB + (((q0_ + 1) ^ (r_ & 15)) << 4);  \
+    _Pragma("unroll") for (int j_ = 0; j_ < BPW; ++j_)                                \
+      S8[j_] = cat8(*reinterpret_cast<const uint4*>(p0_ + j_ * IROWS * RB),           \
+                    *reinterpret_cast<const uint4*>(p1_ + j_ * IROWS * RB));          \
   }
 
   for (int L = 0; L < CONV_LAYERS; ++L) {
@@ -563,14 +556,13 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     // layer loop into ~150 VGPRs
     int n = n_, p1 = p1_, ph0 = ph0_, pw0 = pw0_, ph1 = ph1_, pw1 = pw1_, g = g_;
     asm volatile("" : "+v"(n), "+v"(p1), "+v"(ph0), "+v"(pw0), "+v"(ph1), "+v"(pw1), "+v"(g));
-    // R64: board offsets opaque, so that the compiler does not pair two boards' 8-B reads into
-    // one ds_read2st64_b64 (16-lane bank groups: half ds_read_b64's rate)
-    int bofs[XB] = {0, IROWS * RB, 2 * IROWS * RB, 3 * IROWS * RB};
-    if constexpr (R64) asm volatile("" : "+s"(bofs[0]), "+s"(bofs[1]), "+s"(bofs[2]), "+s"(bofs[3]));
     const int sa_h = sc8[2 * L], sa_l = sc8[2 * L + 1];
-    int sb_l[XB], sb_h[XB];   // the input image's e4m3 units, per board
+    int sb_l[BPW], sb_h[BPW];   // the input image's e4m3 units, per board of the wave
 #pragma unroll
-    for (int bb = 0; bb < XB; ++bb) sb_l[bb] = 127 - (sh[bb] + 11), sb_h[bb] = 127 - sh[bb];
+    for (int j = 0; j < BPW; ++j) {
+      const int shj = pick4(sh, wb0 + j);
+      sb_l[j] = 127 - (shj + 11), sb_h[j] = 127 - shj;
+    }
 #pragma unroll
     for (int p = 0; p < PD; ++p) Z_LOAD_A16(A16[p], p);
 #pragma unroll
@@ -580,44 +572,46 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
     }
     Z_LOAD_B16(B16, 0);
     if constexpr (DIAG_NOLDS) Z_LOAD_B8(B8, 0);
+    {
 #pragma unroll 1
-    for (int s0 = 0; s0 < KBZ; s0 += U) {
+      for (int s0 = 0; s0 < KBZ; s0 += U) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int s = s0 + u;
-        // phase A: Wh x Xh of k-block s on every column tile; meanwhile this step's e4m3
-        // activation fragments and the Wh fragments PD steps ahead
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!DIAG_NOLDS) Z_LOAD_B8(B8, s);
-        Z_LOAD_A16(A16[(u + PD) % RA], s + PD);
+        for (int u = 0; u < U; ++u) {
+          const int s = s0 + u;
+          // phase A: Wh x Xh of k-block s on every column tile; meanwhile this step's e4m3
+          // activation fragments and the Wh fragments PD steps ahead.  Phase B: group s/2 on
+          // square tile s&1; meanwhile the next step's Xh fragments and half of the e4m3 weight
+          // group GD groups ahead
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!DIAG_NOLDS) Z_LOAD_B8(B8, s);
+          Z_LOAD_A16(A16[(u + PD) % RA], s + PD);
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
+          for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-          for (int t = 0; t < 8; ++t)
-            acc[ct * 8 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A16[u % RA][ct], B16[t], acc[ct * 8 + t], 0, 0, 0);
-        // phase B: group s/2 on square tile s&1; meanwhile the next step's Xh fragments and half
-        // of the e4m3 weight group GD groups ahead
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!DIAG_NOLDS) Z_LOAD_B16(B16, s + 1);
-        Z_LOAD_A8(A8[((u >> 1) + GD) % RG], (s >> 1) + GD, (CT / 2) * (u & 1));
-        const int pt = u & 1;
-        const bool term = (u >> 1) & 1;
-        const int sa = term ? sa_l : sa_h;
+            for (int t = 0; t < TW; ++t)
+              acc[ct * TW + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A16[u % RA][ct], B16[t], acc[ct * TW + t], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!DIAG_NOLDS) Z_LOAD_B16(B16, s + 1);
+          Z_LOAD_A8(A8[((u >> 1) + GD) % RG], (s >> 1) + GD, (CT / 2) * (u & 1));
+          const int pt = u & 1;
+          const bool term = (u >> 1) & 1;
+          const int sa = term ? sa_l : sa_h;
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
+          for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-          for (int bb = 0; bb < XB; ++bb) {
-            if constexpr (DIAG_NOB)
-              ;
-            else if constexpr (F6)
-              acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                  A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 2, 2, 0, A8[(u >> 1) % RG][ct][6], 0,
-                  B8[bb][6]);
-            else
-              acc[ct * 8 + bb * 2 + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                  A8[(u >> 1) % RG][ct], B8[bb], acc[ct * 8 + bb * 2 + pt], 0, 0, 0, sa, 0,
-                  term ? sb_h[bb] : sb_l[bb]);
-          }
+            for (int j = 0; j < BPW; ++j) {
+              if constexpr (DIAG_NOB)
+                ;
+              else if constexpr (F6)
+                acc[ct * TW + 2 * j + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    A8[(u >> 1) % RG][ct], B8[j], acc[ct * TW + 2 * j + pt], 2, 2, 0, A8[(u >> 1) % RG][ct][6], 0,
+                    B8[j][6]);
+              else
+                acc[ct * TW + 2 * j + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    A8[(u >> 1) % RG][ct], B8[j], acc[ct * TW + 2 * j + pt], 0, 0, 0, sa, 0,
+                    term ? sb_h[j] : sb_l[j]);
+            }
+        }
       }
     }
     if constexpr (!DIAG_L2 && !DIAG_L1) {
@@ -656,7 +650,7 @@ __global__ __launch_bounds__(64 * zWaves<VAR>, 1) void k_net_z(Dev D, NetWeights
 #undef Z_LOAD_B8
   if (overflow && !DIAG_L2 && !DIAG_L1 && !DIAG_NOB && !DIAG_NOLDS) atomicOr(D.pr.err, ERR_F16);
 
-  heads_reduce<NT, true, TBL>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
+  heads_reduce<NT, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
                          make_float4(__builtin_ldexpf(1.f, -(sh[0] + 11)), __builtin_ldexpf(1.f, -(sh[1] + 11)),
                                      __builtin_ldexpf(1.f, -(sh[2] + 11)), __builtin_ldexpf(1.f, -(sh[3] + 11))));
   stamp(st_heads);
@@ -683,13 +677,11 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
   if (var == 2097152) Z_LAUNCH(2097152, 512);
   else if (var == 8192) Z_LAUNCH(8192, 512);
 #ifdef MTAZ_NET_DIAG
+  else if (var == 4194304) Z_LAUNCH(4194304, 512);
+  else if (var == 4194304 + 8192) Z_LAUNCH(4194304 + 8192, 512);
   // A/B and timing-only builds: the diagnostic library only (tools/bench_net.py --diag)
   else if (var == 1048576) Z_LAUNCH(1048576, 512);
   else if (var == 1048576 + 2048 + 8192) Z_LAUNCH(1048576 + 2048 + 8192, 256);
-  else if (var == 524288) Z_LAUNCH(524288, 512);
-  else if (var == 524288 + 8192) Z_LAUNCH(524288 + 8192, 512);
-  else if (var == 262144) Z_LAUNCH(262144, 512);
-  else if (var == 262144 + 8192) Z_LAUNCH(262144 + 8192, 512);
   else if (var == 16384) Z_LAUNCH(16384, 512);
   else if (var == 32768) Z_LAUNCH(32768, 512);
   else if (var == 65536) Z_LAUNCH(65536, 512);
@@ -698,7 +690,9 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
   else if (var == 8192 + 131072) Z_LAUNCH(8192 + 131072, 512);
   else if (var == 2048 + 8192) Z_LAUNCH(2048 + 8192, 256);
   else if (var == 2048) Z_LAUNCH(2048, 256);
-  else if (var == 4096) Z_LAUNCH(4096, 512);
+  else if (var == 4194304 + 16384) Z_LAUNCH(4194304 + 16384, 512);
+  else if (var == 4194304 + 65536) Z_LAUNCH(4194304 + 65536, 512);
+  else if (var == 4194304 + 131072) Z_LAUNCH(4194304 + 131072, 512);
 #endif
   else Z_LAUNCH(0, 512);
 #undef Z_LAUNCH

@@ -25,21 +25,6 @@ __device__ __forceinline__ int ioff(int part, int bb, int row, int chunk) {
   return part * PARTB + (bb * IROWS + row) * RB + ((chunk ^ (row & 15)) << 4);
 }
 
-// k_net_z VAR 524288: the chunk swizzle as a per-row table (4 bits per row, rows 0..30) chosen
-// by a search over the K loop's ds_read_b128 access pattern (tools/lds_conflicts.py): 5.3 LDS
-// cycles per 16-B read against 6.9 (f16 fragments) and 7.6 (e4m3) for chunk ^ (row & 15)
-constexpr unsigned long long HZ_LO = 0x3c9a4c0739480c73ull, HZ_HI = 0xfc94a7703c94a07ull;
-__device__ __forceinline__ int hz(int row) {
-  const unsigned long long t = row < 16 ? HZ_LO : HZ_HI;
-  return (int)((t >> (4 * (row & 15))) & 15ull);
-}
-template <bool TBL>
-__device__ __forceinline__ int swz(int row) { return TBL ? hz(row) : (row & 15); }
-template <bool TBL>
-__device__ __forceinline__ int ioffs(int part, int bb, int row, int chunk) {
-  return part * PARTB + (bb * IROWS + row) * RB + ((chunk ^ swz<TBL>(row)) << 4);
-}
-
 // image row holding the source square of output square `p` (row ph, file pw) for tap
 // (dh, dw) = (tap/3 - 1, tap%3 - 1), or the zero row (off-board / padding square)
 __device__ __forceinline__ int src_row(int p, int ph, int pw, int tap) {
@@ -107,7 +92,7 @@ __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* po
 // F8LO (k_net_z's image): part 1 holds e4m3 bytes, the lo part of channel c at byte c of the
 // row's first 256 B (16-B chunks swizzled as ioff), board bb's in units of lo_scale[bb] (powers
 // of two).
-template <int NT = 256, bool F8LO = false, bool TBL = false>
+template <int NT = 256, bool F8LO = false>
 __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0, int nb, const NetWeights& W,
                                              int tid, float xscale = 1.f, float4 lo_scale = {1.f, 1.f, 1.f, 1.f}) {
   float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
@@ -118,17 +103,17 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
     const float* wr = o < 2 ? W.pconv_w + o * 256 : W.vconv_w;
     float s = 0.f;
     for (int c = 0; c < 32; ++c) {
-      const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ioffs<TBL>(0, bb, p, c));
+      const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ioff(0, bb, p, c));
       if constexpr (F8LO) {
         const float lsc = bb == 0 ? lo_scale.x : bb == 1 ? lo_scale.y : bb == 2 ? lo_scale.z : lo_scale.w;
-        const uint2 q = *reinterpret_cast<const uint2*>(smem + ioffs<TBL>(1, bb, p, c >> 1) + 8 * (c & 1));
+        const uint2 q = *reinterpret_cast<const uint2*>(smem + ioff(1, bb, p, c >> 1) + 8 * (c & 1));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float lo = __builtin_amdgcn_cvt_f32_fp8((int)((j < 4 ? q.x : q.y) >> (8 * (j & 3))), 0) * lsc;
           s += wr[8 * c + j] * ((float)xh[j] + lo);
         }
       } else {
-        const f16x8 xl = *reinterpret_cast<const f16x8*>(smem + ioffs<TBL>(1, bb, p, c));
+        const f16x8 xl = *reinterpret_cast<const f16x8*>(smem + ioff(1, bb, p, c));
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += wr[8 * c + j] * ((float)xh[j] + (float)xl[j]);
       }

@@ -27,7 +27,7 @@ def read_counters(root):
             for row in csv.DictReader(f):
                 if 'k_net_' not in row.get('Kernel_Name', ''):
                     continue
-                KERNELS.update(re.findall(r'k_net_[xyz]', row['Kernel_Name']))
+                KERNELS.update(re.findall(r'k_net_[yz]', row['Kernel_Name']))
                 key = (path, row['Dispatch_Id'])
                 name = row['Counter_Name']
                 vals[name][key] = vals[name].get(key, 0.0) + float(row['Counter_Value'])
@@ -54,6 +54,10 @@ def main():
     mean = lambda k: sum(c[k]) / len(c[k]) if c.get(k) else None
     fetch_kb, write_kb = mean('FETCH_SIZE'), mean('WRITE_SIZE')
     hit, miss = mean('TCC_HIT_sum'), mean('TCC_MISS_sum')
+    mfma, grbm = mean('SQ_VALU_MFMA_BUSY_CYCLES'), mean('GRBM_GUI_ACTIVE')
+    wave, wait_any, wait_inst, active = (mean('SQ_WAVE_CYCLES'), mean('SQ_WAIT_ANY'), mean('SQ_WAIT_INST_ANY'),
+                                         mean('SQ_ACTIVE_INST_ANY'))
+    conf, ldsact = mean('SQ_LDS_BANK_CONFLICT'), mean('SQ_LDS_IDX_ACTIVE')
     games, sims, line = bench_config(args.root)
     out = {
         'kernel': '+'.join(sorted(KERNELS)),
@@ -63,8 +67,15 @@ def main():
         'write_size_kb_per_launch': write_kb,
         'hbm_bytes_per_launch': (2 * fetch_kb + write_kb) * 1024 if fetch_kb is not None and write_kb is not None else None,
         'l2_hit_rate': hit / (hit + miss) if hit is not None and miss else None,
-        'method': 'rocprofv3 --pmc, one pass per counter group, --kernel-include-regex k_net_[xyz]; '
-                  'bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE half-count correction)',
+        # MFMA pipe busy per SIMD (SQ_VALU_MFMA_BUSY_CYCLES over the chip's 1024 SIMDs) over the
+        # kernel's cycles per XCD (GRBM_GUI_ACTIVE sums the 8 XCDs)
+        'mfma_busy_frac': (mfma / 1024) / (grbm / 8) if mfma is not None and grbm else None,
+        'sq_wave_cycle_shares': ({'active_inst_any': active / wave, 'wait_inst_any': wait_inst / wave,
+                                  'wait_any': wait_any / wave} if wave else None),
+        'lds_bank_conflict_frac': conf / ldsact if conf is not None and ldsact else None,
+        'method': 'rocprofv3 --pmc, one pass per counter group, --kernel-include-regex k_net_[yz]; '
+                  'bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE half-count correction); '
+                  'mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs)',
     }
     if line is not None:
         out['boards_per_launch'] = line['roofline']['flop_per_launch'] / 638245892
