@@ -109,7 +109,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // 2097152: the e4m3 epilogue's unfused form (product: v_fma_mix for the lo part, the Xh copy and
   // the residual seed; bit-identical, test_gpu_net.py test_z_mix_epilogue_bit_identical)
   constexpr bool NOMIX = (VAR & 2097152) != 0;
-  __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
+  __shared__ __attribute__((aligned(16))) char smem[ZIMGB + AUXB];
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
   if (b0 >= nb) return;
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   float mxb[XB], mxblk[XB];
 #pragma unroll
   for (int bb = 0; bb < XB; ++bb) mxb[bb] = W.yrange[2 * CONV_LAYERS + 2], mxblk[bb] = 0.f;
-  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMGB + AUXB - 4 * 2 * XB);   // [slot 2][board]
+  unsigned* mxs = reinterpret_cast<unsigned*>(smem + ZIMGB + AUXB - 4 * 2 * XB);   // [slot 2][board]
   if (tid < 2 * XB) mxs[tid] = 0u;
   int slot = 0;
   // e4m3 exponents of board bb's current image: Xh8 = e4m3(Xh * 2^sh[bb]),
@@ -226,9 +226,9 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         f32x4v& a = acc[ct * TW + t];
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
-          const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1);
-          const int al8 = ioff(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
-          const int ah8 = ioff(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
+          const int ah = zoff(0, bb, p, co0 >> 3) + 8 * (g & 1);
+          const int al8 = zoff(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
+          const int ah8 = zoff(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
           float y[4];
           y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
           y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         bv[ct] = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
       }
       // byte address of byte `b` of block blk's slot of term `term` on row p of board bb
-      auto baddr = [&](int term, int bb, int p, int b) { return ioff(1, bb, p, 16 * term + 2 * blk + (b >> 4)) + (b & 15); };
+      auto baddr = [&](int term, int bb, int p, int b) { return zoff(1, bb, p, 16 * term + 2 * blk + (b >> 4)) + (b & 15); };
   #pragma unroll
       for (int t = 0; t < TW; ++t) {
         const int j = t >> 1, bb = wb0 + j, pt = t & 1;
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
               const uint32_t c = ct ? B24 : A24;
               uint32_t e = (c & 0x3fu) | ((c << 2) & 0x3f00u) | ((c << 4) & 0x3f0000u) | ((c << 6) & 0x3f000000u);
               e = (e & 0x1f1f1f1fu) | ((e & 0x20202020u) << 2);
-              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ioff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1));
+              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + zoff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1));
               xin[4 * ct + 0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 0) * lsc);
               xin[4 * ct + 1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 1) * lsc);
               xin[4 * ct + 2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 2) * lsc);
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         if (valid) {
   #pragma unroll
           for (int ct = 0; ct < 2; ++ct)
-            *reinterpret_cast<f16x4*>(smem + ioff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
+            *reinterpret_cast<f16x4*>(smem + zoff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
         }
   #pragma unroll
         for (int term = 0; term < 2; ++term) {
@@ -431,9 +431,9 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   };
 
   // ---------------- stem: conv3x3 8->256 in f16x3 (k_net_y's), K = 3 k-blocks -------------
-  // (stem_input zeroes both parts' zero rows, which covers [Xl8 | Xh8] of the zero row)
-  char* simg = smem + IMGB;
-  stem_input<NT>(smem, simg, pos, b0, nb, W, tid);
+  // (stem_input zeroes both parts' zero lines, which covers [Xl8 | Xh8] of off-board taps)
+  char* simg = smem + ZIMGB;
+  stem_input<NT, true>(smem, simg, pos, b0, nb, W, tid);
   __syncthreads();
   {
     const uint4* Ws = W.stemy + (size_t)(CT * wc) * 3 * 128 + lane;
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   const uint4* W8 = W.conv8 + (size_t)(CT * wc) * GZ * 128 + lane;
   const uint4* W6 = W.conv6 + (size_t)(CT * wc) * GZ * 112;
   const int32_t* sc8 = W.conv8_sc;
-  const int bofs = wb0 * IROWS * RB;   // the wave's first board in each image part
+  const int bofs = wb0 * ZBOARD;   // the wave's first board in each image part
 
   // Wh fragments of step (k-block) KB, the wave's channel tiles
 #define Z_LOAD_A16(S, KB)                                                             \
@@ -525,11 +525,9 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   {                                                                                   \
     const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
     const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
-    const int r0_ = src_row(n, ph0, pw0, tap_), r1_ = src_row(p1, ph1, pw1, tap_);    \
-    const int o0_ = r0_ * RB + ((ch_ ^ (r0_ & 15)) << 4);                             \
-    const int o1_ = r1_ * RB + ((ch_ ^ (r1_ & 15)) << 4);                             \
+    const int o0_ = zsrc(n, ph0, pw0, tap_, ch_), o1_ = zsrc(p1, ph1, pw1, tap_, ch_); \
     _Pragma("unroll") for (int j_ = 0; j_ < BPW; ++j_) {                              \
-      const char* base_ = smem + bofs + j_ * IROWS * RB;                              \
+      const char* base_ = smem + bofs + j_ * ZBOARD;                                  \
       S16[2 * j_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                     \
       S16[2 * j_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);                 \
     }                                                                                 \
@@ -540,14 +538,15 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   {                                                                                   \
     const int kk_ = (KB) < KBZ ? (KB) : KBZ - 1;                                      \
     const int tap_ = kk_ >> 3, term_ = (kk_ >> 1) & 1, cc_ = (kk_ >> 2) & 1;          \
-    const int r_ = (kk_ & 1) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_); \
     const int q0_ = 16 * term_ + 8 * cc_ + 2 * g;                                     \
-    /* part-1 row base once, so that the boards' offsets (< 64 KB) fit the ds_read immediate */ \
-    const char* p0_ = smem + PARTB + bofs + r_ * RB + ((q0_ ^ (r_ & 15)) << 4);        \
-    const char* p1_ = smem + PARTB + bofs + r_ * RB + (((q0_ + 1) ^ (r_ & 15)) << 4);  \
+    /* part-1 row base once, so that the boards' offsets (< 64 KB) fit the ds_read immediate; */ \
+    /* chunk q0 + 1 is 256 B after chunk q0 (zero-line cells: the same cell) */    \
+    const int z0_ = (kk_ & 1) ? zsrc(p1, ph1, pw1, tap_, q0_) : zsrc(n, ph0, pw0, tap_, q0_); \
+    const char* p0_ = smem + ZPART + bofs + z0_;                                      \
+    const char* p1_ = p0_ + (z0_ < ZROWS_B ? 256 : 0);                                \
     _Pragma("unroll") for (int j_ = 0; j_ < BPW; ++j_)                                \
-      S8[j_] = cat8(*reinterpret_cast<const uint4*>(p0_ + j_ * IROWS * RB),           \
-                    *reinterpret_cast<const uint4*>(p1_ + j_ * IROWS * RB));          \
+      S8[j_] = cat8(*reinterpret_cast<const uint4*>(p0_ + j_ * ZBOARD),               \
+                    *reinterpret_cast<const uint4*>(p1_ + j_ * ZBOARD));              \
   }
 
   for (int L = 0; L < CONV_LAYERS; ++L) {
@@ -650,7 +649,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
 #undef Z_LOAD_B8
   if (overflow && !DIAG_L2 && !DIAG_L1 && !DIAG_NOB && !DIAG_NOLDS) atomicOr(D.pr.err, ERR_F16);
 
-  heads_reduce<NT, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
+  heads_reduce<NT, true, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
                          make_float4(__builtin_ldexpf(1.f, -(sh[0] + 11)), __builtin_ldexpf(1.f, -(sh[1] + 11)),
                                      __builtin_ldexpf(1.f, -(sh[2] + 11)), __builtin_ldexpf(1.f, -(sh[3] + 11))));
   stamp(st_heads);
@@ -664,7 +663,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
       stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
     }
   }
-  heads_out(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
+  heads_out<true>(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
 }
 
 template <bool S>

@@ -25,6 +25,32 @@ __device__ __forceinline__ int ioff(int part, int bb, int row, int chunk) {
   return part * PARTB + (bb * IROWS + row) * RB + ((chunk ^ (row & 15)) << 4);
 }
 
+// k_net_z's image layout.  Per part and board, rows 0..31 x 32 chunks of 16 B, stored chunk-major
+// within 16-row halves: (row r, chunk q) at 256 (q + 32 (r >> 4)) + 16 (r & 15).  The bank group
+// of a 16-B chunk then depends on its row alone, and a K-loop fragment read (each 16-lane read
+// group = the 16 consecutive output squares of a tile, any chunk per lane) touches 16 distinct
+// rows: conflict-free.  Off-board taps read a per-lane cell of the board's zero line (256 B after
+// the rows), on the bank the on-board source would have had (tools/lds_conflicts.py: 4.0 LDS
+// cycles per ds_read_b128 against 6.9 / 7.6 for the row-major swizzled image).
+constexpr int ZROWS_B = 16384;                 // bytes of rows per board and part
+constexpr int ZBOARD = ZROWS_B + 256;          // + the zero line
+constexpr int ZPART = XB * ZBOARD;             // 66,560 B per part
+constexpr int ZIMGB = 2 * ZPART;               // 133,120 B
+__device__ __forceinline__ int zrow(int row, int chunk) { return 256 * (chunk + 32 * (row >> 4)) + 16 * (row & 15); }
+__device__ __forceinline__ int zoff(int part, int bb, int row, int chunk) {
+  return part * ZPART + bb * ZBOARD + zrow(row, chunk);
+}
+// byte offset within a board of the 16-B chunk `chunk` of the source square of output square p
+// (row ph, file pw) for tap (dh, dw), or of p's cell in the zero line when the tap is off-board
+__device__ __forceinline__ int zsrc(int p, int ph, int pw, int tap, int chunk) {
+  const int dh = tap / 3 - 1, dw = tap - 3 * (tap / 3) - 1;
+  const int r = ph + dh, c = pw + dw, s = p + 5 * dh + dw;
+  // bitwise, not short-circuit: a select (v_cndmask), not exec-masked branches
+  const bool valid = (p < 30) & ((unsigned)r < 6u) & ((unsigned)c < 5u);
+  const int on = zrow(s, chunk), off = ZROWS_B + 16 * (s & 15);
+  return valid ? on : off;
+}
+
 // image row holding the source square of output square `p` (row ph, file pw) for tap
 // (dh, dw) = (tap/3 - 1, tap%3 - 1), or the zero row (off-board / padding square)
 __device__ __forceinline__ int src_row(int p, int ph, int pw, int tap) {
@@ -50,12 +76,19 @@ __device__ __forceinline__ float clock_of(const Pos& p) {
 // [part][board][row 31][8 ch f16], channel c = plane*4 + e of Embedding(7,4) applied to the
 // own / opponent token planes (exp/policy.py:71-74, encoder exp/environment.py:63-75).
 // Caller: __syncthreads() before reading.
-template <int NT = 256>
+template <int NT = 256, bool ZL = false>
 __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* pos, int b0, int nb,
                                            const NetWeights& W, int tid) {
-  for (int i = tid; i < 2 * XB * 32; i += NT) {
-    const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
-    *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
+  if constexpr (ZL) {   // the zero lines
+    for (int i = tid; i < 2 * XB * 16; i += NT) {
+      const int part = i / (XB * 16), bb = (i / 16) % XB, c = i & 15;
+      *reinterpret_cast<uint4*>(smem + part * ZPART + bb * ZBOARD + ZROWS_B + 16 * c) = make_uint4(0, 0, 0, 0);
+    }
+  } else {
+    for (int i = tid; i < 2 * XB * 32; i += NT) {
+      const int part = i / (XB * 32), bb = (i / 32) % XB, ch = i & 31;
+      *reinterpret_cast<uint4*>(smem + ioff(part, bb, ZROW, ch)) = make_uint4(0, 0, 0, 0);
+    }
   }
   for (int i = tid; i < 2 * XB * IROWS; i += NT) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
@@ -92,10 +125,11 @@ __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* po
 // F8LO (k_net_z's image): part 1 holds e4m3 bytes, the lo part of channel c at byte c of the
 // row's first 256 B (16-B chunks swizzled as ioff), board bb's in units of lo_scale[bb] (powers
 // of two).
-template <int NT = 256, bool F8LO = false>
+template <int NT = 256, bool F8LO = false, bool ZL = false>
 __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0, int nb, const NetWeights& W,
                                              int tid, float xscale = 1.f, float4 lo_scale = {1.f, 1.f, 1.f, 1.f}) {
-  float* fp = reinterpret_cast<float*>(smem + IMGB);   // [XB][64]: pconv features (60) + clock
+  auto off = [](int part, int bb, int row, int chunk) { return ZL ? zoff(part, bb, row, chunk) : ioff(part, bb, row, chunk); };
+  float* fp = reinterpret_cast<float*>(smem + (ZL ? ZIMGB : IMGB));   // [XB][64]: pconv features (60) + clock
   float* fv = fp + XB * 64;                            // [XB][32]: vconv features (30) + clock
   float* red = fv + XB * 32;                           // [XB][256]
   for (int t = tid; t < XB * 90; t += NT) {
@@ -103,17 +137,17 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
     const float* wr = o < 2 ? W.pconv_w + o * 256 : W.vconv_w;
     float s = 0.f;
     for (int c = 0; c < 32; ++c) {
-      const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ioff(0, bb, p, c));
+      const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + off(0, bb, p, c));
       if constexpr (F8LO) {
         const float lsc = bb == 0 ? lo_scale.x : bb == 1 ? lo_scale.y : bb == 2 ? lo_scale.z : lo_scale.w;
-        const uint2 q = *reinterpret_cast<const uint2*>(smem + ioff(1, bb, p, c >> 1) + 8 * (c & 1));
+        const uint2 q = *reinterpret_cast<const uint2*>(smem + off(1, bb, p, c >> 1) + 8 * (c & 1));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float lo = __builtin_amdgcn_cvt_f32_fp8((int)((j < 4 ? q.x : q.y) >> (8 * (j & 3))), 0) * lsc;
           s += wr[8 * c + j] * ((float)xh[j] + lo);
         }
       } else {
-        const f16x8 xl = *reinterpret_cast<const f16x8*>(smem + ioff(1, bb, p, c));
+        const f16x8 xl = *reinterpret_cast<const f16x8*>(smem + off(1, bb, p, c));
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += wr[8 * c + j] * ((float)xh[j] + (float)xl[j]);
       }
@@ -149,9 +183,10 @@ __device__ __forceinline__ void heads_reduce(char* smem, const Pos* pos, int b0,
 // Heads, part 2 (wave bb finishes board bb): value = tanh, then either the full 554 logits
 // (evaluate mode) or the leaf priors = softmax over the legal moves' logits in the node's
 // legal-list order (exp/agent.py:67-69), written to D.lf.
+template <bool ZL = false>
 __device__ __forceinline__ void heads_out(const Dev& D, char* smem, int b0, int nb, const NetWeights& W, int mode,
                                           float* logits_out, float* values_out, int wave, int lane) {
-  const float* fp = reinterpret_cast<const float*>(smem + IMGB);
+  const float* fp = reinterpret_cast<const float*>(smem + (ZL ? ZIMGB : IMGB));
   const float* red = fp + XB * 64 + XB * 32;
   if (wave >= XB) return;
   const int bb = wave;

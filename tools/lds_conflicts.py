@@ -13,8 +13,13 @@ the source row of output square n (tile 0) or 16 + n (tile 1) for the step's tap
 for off-board taps), chunk 4 (kk & 7) + g (f16 fragments) or the chunk pair
 16 term + 8 cc + 2 g + {0, 1} (e4m3 / e2m3 fragments).
 
-  python tools/lds_conflicts.py            # cycles per 16-B read: row & 15 vs the table
-  python tools/lds_conflicts.py --search 4 # anneal a table (seed 4 gave the committed one)
+  python tools/lds_conflicts.py            # cycles per 16-B read: row & 15, the table, the z layout
+  python tools/lds_conflicts.py --search 4 # anneal a table (seed 4 gave round 1's table)
+
+Round 2 (net_common.h zoff / zsrc, k_net_z's image since): chunk-major 16-row halves, (row r,
+chunk q) at 256 (q + 32 (r >> 4)) + 16 (r & 15), off-board taps on a per-lane cell of a zero line:
+the bank depends on the row alone, 4.0 cycles per read (conflict-free), measured -3% K-loop
+cycles (e4m3) and -7% (e2m3) against the row-major image (profiles/r02/).
 
 Measured (bench_net, profiles/r01_z2/): the table cut the model's cycles per read from 7.2 to
 5.3 and SQ_LDS_BANK_CONFLICT accordingly, but not the K loop's time (+2% e4m3, -4% e2m3), and
@@ -55,6 +60,38 @@ def patterns():
             pats.append(('f8', [(src_row((l & 15) + 16 * (kk & 1), tap), 16 * term + 8 * cc + 2 * (l >> 4) + half)
                                 for l in range(64)]))
     return pats
+
+
+def zaddr(r, q, p, tap):
+    """byte address in the z layout (off-board taps: the lane's zero-line cell)"""
+    if r == ZROW:
+        dh, dw = tap // 3 - 1, tap % 3 - 1
+        return 1 << 20 | 16 * ((p + 5 * dh + dw) & 15)
+    return 256 * (q + 32 * (r >> 4)) + 16 * (r & 15)
+
+
+def z_cycles():
+    """cycles per ds_read_b128 of the K loop's f16 / e4m3 fragment reads in the z layout"""
+    def cyc(addrs):
+        tot = 0
+        for grp in G128:
+            banks = {}
+            for l in grp:
+                banks.setdefault((addrs[l] // 16) & 15, set()).add(addrs[l])
+            tot += max(len(s) for s in banks.values())
+        return tot
+    f16, f8 = [], []
+    for kk in range(72):
+        tap, ch = kk >> 3, 4 * (kk & 7)
+        for pt in (0, 1):
+            f16.append(cyc([zaddr(src_row((l & 15) + 16 * pt, tap), ch + (l >> 4), (l & 15) + 16 * pt, tap)
+                            for l in range(64)]))
+        term, cc = (kk >> 1) & 1, (kk >> 2) & 1
+        for half in (0, 1):
+            p0 = lambda l: (l & 15) + 16 * (kk & 1)
+            f8.append(cyc([zaddr(src_row(p0(l), tap), 16 * term + 8 * cc + 2 * (l >> 4) + half, p0(l), tap)
+                           for l in range(64)]))
+    return sum(f16) / len(f16), sum(f8) / len(f8)
 
 
 def read_cycles(h, pat):
@@ -103,6 +140,7 @@ def main():
     pats = patterns()
     print('row & 15 :', score([r & 15 for r in range(IROWS)], pats))
     print('table    :', score(TABLE, pats))
+    print('z layout :', z_cycles())
     if a.search is not None:
         c, h = search(a.search, a.iters, pats)
         print('searched :', score(h, pats), h)
