@@ -53,7 +53,11 @@ struct Games {
   int32_t* outcome;       // game result (Outcome)
   int32_t* root_new;      // root absent from the agent's table at move start
   int32_t* root_k;        // legal-list length of the root
-  int64_t* noise_off;     // this move's Dirichlet vectors: noise[noise_off[g] + j*k + c]
+  // this move's Dirichlet vectors: draw j of game g at noise[noise_off[g] + j*noise_js[g] + c]
+  // (mtaz_set_noise: per-game contiguous, js = k; mtaz_play: draw-major, js = the move's total k,
+  // so that a range of draws is one contiguous upload)
+  int64_t* noise_off;
+  int32_t* noise_js;
   double* noise;
   uint32_t* path_node;    // [G*DMAX] chain of (node, edge) of the current sim
   uint32_t* path_edge;

@@ -395,7 +395,7 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
     const double* noise = nullptr;
     if (root) {
       const int j = sim - D.gm.root_new[g];
-      noise = D.gm.noise + D.gm.noise_off[g] + (int64_t)j * k;
+      noise = D.gm.noise + D.gm.noise_off[g] + (int64_t)j * D.gm.noise_js[g];
     }
     double best_u = -__builtin_inf();
     int best_i = 0x7fffffff;

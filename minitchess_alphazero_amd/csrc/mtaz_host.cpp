@@ -521,6 +521,9 @@ struct mtaz_engine {
   double* d_sqrt = nullptr;
   int count_log_cap = 0;
   size_t noise_cap = 0;
+  double* noise_host = nullptr;         // pinned staging of mtaz_play's draw-major noise
+  size_t noise_host_cap = 0;
+  std::vector<int32_t> last_root_k;     // root legal counts of the last mtaz_move_begin
   std::vector<MTState> rng;
   std::vector<std::vector<PlyRec>> rec;
   std::vector<int32_t> final_outcome;
@@ -548,6 +551,7 @@ struct mtaz_engine {
   ~mtaz_engine() {
     for (mtaz_engine* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
+    if (noise_host) (void)hipHostFree(noise_host);
     for (auto e : ev) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
@@ -607,6 +611,7 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&gm.root_new, G));
   ECHK(h->dalloc(&gm.root_k, G));
   ECHK(h->dalloc(&gm.noise_off, G));
+  ECHK(h->dalloc(&gm.noise_js, G));
   ECHK(h->dalloc(&gm.path_node, (size_t)G * gm.DMAX));
   ECHK(h->dalloc(&gm.path_edge, (size_t)G * gm.DMAX));
   ECHK(h->dalloc(&gm.path_len, G));
@@ -1217,7 +1222,9 @@ extern "C" int mtaz_move_begin(mtaz_engine* h, int32_t* root_k, int32_t* root_ne
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(root_k, h->d.gm.root_k, h->G * 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(root_new, h->d.gm.root_new, h->G * 4, hipMemcpyDeviceToHost, h->stream));
-  return check_err(h);
+  const int rc = check_err(h);   // (synchronises the stream)
+  h->last_root_k.assign(root_k, root_k + h->G);
+  return rc;
 }
 
 extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, int64_t total) {
@@ -1232,6 +1239,10 @@ extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t
   }
   if (total > 0) HIPCHK(hipMemcpyAsync(h->d.gm.noise, noise, total * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offsets, h->G * 8, hipMemcpyHostToDevice, h->stream));
+  // per-game contiguous draws: draw stride = the game's root legal count (mtaz_move_begin)
+  std::vector<int32_t> js(h->G, 0);
+  for (int g = 0; g < h->G && g < (int)h->last_root_k.size(); ++g) js[g] = h->last_root_k[g];
+  HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -1481,7 +1492,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   std::vector<int32_t> agents(G), outcome_v(G), root_k(G), root_new(G), actions(G, 0);
   std::vector<uint32_t> roots((size_t)G * 5);
   std::vector<int64_t> offs(G);
-  std::vector<double> noise;
+  std::vector<int32_t> js(G);
   std::vector<uint16_t> codes((size_t)G * KMAX);
   std::vector<uint32_t> visits((size_t)G * KMAX);
   ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
@@ -1503,23 +1514,57 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     double ts = now_ms();
     ECHK(mtaz_move_begin(h, root_k.data(), root_new.data()));
     sync_ms += now_ms() - ts;
-    // Dirichlet draws: sims - root_new vectors of size k per active game
+    // Dirichlet draws: sims - root_new vectors of size k per active game, draw-major (draw j of
+    // every game in one block of K = sum k), generated and uploaded in chunks of NCH draws so
+    // that the host draws chunk c + 1 while the GPU runs the simulations of chunk c.  Each
+    // game's generator still runs its draws in order (exp/agent.py:82), so the streams are
+    // unchanged.
     double tr = now_ms();
-    int64_t total = 0;
+    int64_t K = 0;
     for (int g = 0; g < G; ++g) {
-      offs[g] = total;
-      if (active[g]) total += (int64_t)(h->sims - root_new[g]) * root_k[g];
+      offs[g] = K;
+      if (active[g]) K += root_k[g];
     }
-    noise.resize(std::max<int64_t>(total, 1));
-    parallel_for(G, [&](int g) {
-      if (!active[g]) return;
-      const int k = root_k[g];
-      double* out = noise.data() + offs[g];
-      for (int j = 0; j < h->sims - root_new[g]; ++j) legacy_dirichlet(h->rng[g], h->alpha, k, out + (size_t)j * k);
-    });
+    const size_t need = (size_t)std::max<int64_t>(K, 1) * h->sims;
+    if (need > h->noise_cap) {
+      void* q = nullptr;
+      HIPCHK(hipMalloc(&q, need * 8));
+      h->allocs.push_back(q);
+      h->d.gm.noise = (double*)q;
+      h->noise_cap = need;
+    }
+    if (need > h->noise_host_cap) {
+      if (h->noise_host) HIPCHK(hipHostFree(h->noise_host));
+      HIPCHK(hipHostMalloc(&h->noise_host, need * 8, hipHostMallocDefault));
+      h->noise_host_cap = need;
+    }
+    for (int g = 0; g < G; ++g) js[g] = (int32_t)K;
+    HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs.data(), G * 8, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), G * 4, hipMemcpyHostToDevice, h->stream));
+    constexpr int NCH = 8;
+    auto draw_chunk = [&](int j0) {   // draws [j0, j0 + NCH) of every active game
+      parallel_for(G, [&](int g) {
+        if (!active[g]) return;
+        const int k = root_k[g], jn = std::min(j0 + NCH, h->sims - root_new[g]);
+        for (int j = j0; j < jn; ++j) legacy_dirichlet(h->rng[g], h->alpha, k, h->noise_host + (size_t)j * K + offs[g]);
+      });
+      const int jn = std::min(j0 + NCH, h->sims);
+      if (jn > j0 && K > 0)
+        HIPCHK(hipMemcpyAsync(h->d.gm.noise + (size_t)j0 * K, h->noise_host + (size_t)j0 * K, (size_t)(jn - j0) * K * 8,
+                              hipMemcpyHostToDevice, h->stream));
+      return 0;
+    };
+    ECHK(draw_chunk(0));
     rng_ms += now_ms() - tr;
-    ECHK(mtaz_set_noise(h, noise.data(), offs.data(), total));
-    for (int s = 0; s < h->sims; ++s) ECHK(sim_gpu(h, s));
+    for (int s0 = 0; s0 < h->sims; s0 += NCH) {
+      // simulation s uses draw s - root_new <= s: chunk s0 / NCH is on the stream before them
+      for (int s = s0; s < std::min(s0 + NCH, h->sims); ++s) ECHK(sim_gpu(h, s));
+      if (s0 + NCH < h->sims) {
+        tr = now_ms();
+        ECHK(draw_chunk(s0 + NCH));
+        rng_ms += now_ms() - tr;
+      }
+    }
     ts = now_ms();
     ECHK(mtaz_move_end(h, codes.data(), visits.data(), nullptr, KMAX));
     sync_ms += now_ms() - ts;
