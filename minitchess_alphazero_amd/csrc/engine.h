@@ -68,6 +68,11 @@ struct Games {
 };
 
 struct Leaves {
+  // k_select writes game g's leaf (node, position) at index g, NONE when the simulation ended
+  // without one; k_leaf_compact then lists the leaves densely in game order (no contended
+  // counter: one atomic per game on a single address serialised the select kernel)
+  uint32_t* gnode;        // [G]
+  Pos* gpos;              // [G]
   int32_t* count;         // [1]
   int32_t* game;          // [G]
   int32_t* tree;          // [G]
@@ -174,6 +179,9 @@ void launch_replay_put(const Pos* pos, const int32_t* k, const int64_t* e0, cons
 void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s);
 void launch_move_begin(const Dev& d, hipStream_t s);
 void launch_select(const Dev& d, int sim, hipStream_t s);
+#ifdef MTAZ_NET_DIAG
+int diag_select_stamps(unsigned long long* out8, int reset);   // k_select phase cycles (diag library)
+#endif
 void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const Pos* pos, const int32_t* count, int max_b,
                 int mode, float* values_out, hipStream_t s, hipEvent_t trunk_begin, hipEvent_t trunk_end);
 // fused fp16x3 network (stem + 18 convs + heads in one launch, 4 boards per workgroup):

@@ -8,6 +8,8 @@
 //   * network kernels    embedding+stem, 18 residual 3x3 convs on fp32 MFMA
 //                        (v_mfma_f32_32x32x2_f32, exact f32 products), fused heads
 //                        with a legal-only softmax (exp/policy.py:71-80, exp/agent.py:67-69)
+#include <vector>
+
 #include "engine.h"
 
 namespace mtaz {
@@ -40,46 +42,72 @@ __device__ __forceinline__ BB dev_apply_code(const BB& b, int code) {
   return make_move(b, from, to, promo);
 }
 
-// Sorted legal codes with duplicates (exp/environment.py:48-50) computed by one wave:
-// lane s < 30 owns the piece on square s, generates its legal targets, the wave
-// prefix-sums the per-lane counts, scatters the codes to LDS and ranks them.
+// The rule tables (knight / king / pawn attacks, rays: 1,444 B) copied into the workgroup's LDS:
+// move generation looks them up per lane with lane-varying squares, which from the constant
+// bank are vector loads through the texture path (tools/select_stamps.py: 58% of k_select's
+// cycles went to move generation with the tables there).  Call with all lanes, then barrier.
+__device__ __forceinline__ void load_rules_lds(RuleTables* s_rt) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&d_rules);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(s_rt);
+  for (int i = threadIdx.x; i < (int)(sizeof(RuleTables) / 4); i += blockDim.x) dst[i] = src[i];
+}
+
+// LDS scratch of one wave's move generation
+struct LegalLds {
+  uint16_t raw[KMAX], sorted[KMAX];
+  uint16_t pm[KMAX];            // pseudo moves from | to << 8 (at most 15 x 15 = 225 < KMAX)
+};
+
+// Sorted legal codes with duplicates (exp/environment.py:48-50) computed by one wave, lane-parallel
+// over pseudo moves: lane s < 30 lists the pseudo targets of its piece, the wave prefix-sums them
+// into one list, then each lane tests one pseudo move (own king not attacked after it: the
+// oracle's Board._gen_legal), and the legal ones are scattered with their multiplicity (a pawn
+// reaching the last rank is listed once per promotion piece) and ranked by code.  The list is a
+// sorted multiset, so it does not depend on the order the moves are found in.
 // Must be called by all 64 lanes in uniform control flow.  Returns k or -1 (> KMAX).
-__device__ int wave_legal(const BB& b, uint32_t flags, uint16_t* s_raw, uint16_t* s_sorted) {
+__device__ int wave_legal(const BB& b, uint32_t flags, const RuleTables& RT, LegalLds& L) {
   const int lane = threadIdx.x & 63;
   const uint32_t own = b.white ? b.w : b.b;
   const int side = b.white ? 0 : 1;
-  uint32_t tg = 0;
-  int cnt = 0;
-  if (lane < NSQ && ((own >> lane) & 1u)) {
-    tg = legal_targets(b, lane, flags);
-    uint32_t m = tg;
-    while (m) {
-      const int to = lsb(m);
-      m &= m - 1;
-      cnt += move_mult(b, lane, to, flags);
-    }
-  }
+  uint32_t ps = 0;
+  if (lane < NSQ && ((own >> lane) & 1u)) ps = pseudo_targets(b, lane, flags, RT);
+  const int cnt = popc(ps);
   const int incl = wave_incl_scan(cnt);
-  const int total = __shfl(incl, 63, 64);
-  if (total > KMAX) return -1;
+  const int nps = __shfl(incl, 63, 64);     // <= 15 * 15: own pieces x other squares
   int off = incl - cnt;
-  uint32_t m = tg;
-  while (m) {
-    const int to = lsb(m);
-    m &= m - 1;
-    const uint16_t code = (uint16_t)d_codec.enc[side][lane * 30 + to];
-    const int mult = move_mult(b, lane, to, flags);
-    for (int r = 0; r < mult; ++r) s_raw[off++] = code;
+  for (uint32_t m = ps; m; m &= m - 1) L.pm[off++] = (uint16_t)(lane | (lsb(m) << 8));
+  __syncthreads();
+  const int ksq0 = king_sq(b, b.white);
+  int total = 0;
+  for (int base = 0; base < nps; base += 64) {
+    const int i = base + lane;
+    int mult = 0, code = 0;
+    if (i < nps) {
+      const int from = L.pm[i] & 0xff, to = L.pm[i] >> 8;
+      BB n = b;
+      clear_sq(n, (1u << from) | (1u << to));
+      set_piece(n, to, piece_type_at(b, from), b.white);
+      const int k = ((b.king >> from) & 1u) ? to : ksq0;
+      if (k < 0 || !attacked(n, k, !b.white, RT)) {
+        mult = move_mult(b, from, to, flags);
+        code = d_codec.enc[side][from * 30 + to];
+      }
+    }
+    const int mincl = wave_incl_scan(mult);
+    int o = total + mincl - mult;
+    total += __shfl(mincl, 63, 64);
+    if (total > KMAX) return -1;
+    for (int r = 0; r < mult; ++r) L.raw[o++] = (uint16_t)code;
   }
   __syncthreads();
   for (int j = lane; j < total; j += 64) {
-    const uint16_t c = s_raw[j];
+    const uint16_t c = L.raw[j];
     int rank = 0;
     for (int i = 0; i < total; ++i) {
-      const uint16_t o = s_raw[i];
+      const uint16_t o = L.raw[i];
       rank += (o < c) || (o == c && i < j);
     }
-    s_sorted[rank] = c;
+    L.sorted[rank] = c;
   }
   __syncthreads();
   return total;
@@ -108,26 +136,29 @@ __device__ int legal_count(const BB& b, uint32_t flags) {
 __global__ __launch_bounds__(64) void k_legal_batch(const Pos* __restrict__ pos, int n, uint32_t flags, int move_cap,
                                                     uint16_t* __restrict__ codes, int32_t* __restrict__ counts,
                                                     uint32_t* __restrict__ masks, int32_t* __restrict__ outcomes) {
-  __shared__ uint16_t s_raw[KMAX], s_sorted[KMAX];
+  __shared__ LegalLds s_l;
+  __shared__ RuleTables s_rt;
   __shared__ uint32_t s_mask[MASK_WORDS];
   const int i = blockIdx.x, lane = threadIdx.x;
   if (i >= n) return;
+  load_rules_lds(&s_rt);
   const BB b = unpack(pos[i]);
   if (lane < MASK_WORDS) s_mask[lane] = 0;
-  const int k = wave_legal(b, flags, s_raw, s_sorted);
+  __syncthreads();
+  const int k = wave_legal(b, flags, s_rt, s_l);
   if (k < 0) {
     if (lane == 0) { counts[i] = -1; outcomes[i] = -1; }
     return;
   }
   for (int j = lane; j < k; j += 64) {
-    codes[(size_t)i * KMAX + j] = s_sorted[j];
-    atomicOr(&s_mask[s_sorted[j] >> 5], 1u << (s_sorted[j] & 31));
+    codes[(size_t)i * KMAX + j] = s_l.sorted[j];
+    atomicOr(&s_mask[s_l.sorted[j] >> 5], 1u << (s_l.sorted[j] & 31));
   }
   __syncthreads();
   if (lane < MASK_WORDS) masks[(size_t)i * MASK_WORDS + lane] = s_mask[lane];
   if (lane == 0) {
     counts[i] = k;
-    outcomes[i] = outcome(b, k, in_check(b), flags, move_cap, 1);
+    outcomes[i] = outcome(b, k, in_check(b, s_rt), flags, move_cap, 1, s_rt);
   }
 }
 
@@ -277,7 +308,8 @@ void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStrea
 // Move start: does the agent's table already hold the root (exp/agent.py:57)?  The host
 // needs k and "root is new" to draw exactly sims - root_new Dirichlet vectors (:81-82).
 __global__ __launch_bounds__(64) void k_move_begin(Dev D) {
-  __shared__ uint16_t s_raw[KMAX], s_sorted[KMAX];
+  __shared__ LegalLds s_l;
+  __shared__ RuleTables s_rt;
   const int g = blockIdx.x, lane = threadIdx.x;
   if (!D.gm.active[g]) {
     if (lane == 0) { D.gm.root_k[g] = 0; D.gm.root_new[g] = 0; }
@@ -294,8 +326,10 @@ __global__ __launch_bounds__(64) void k_move_begin(Dev D) {
     }
     return;
   }
+  load_rules_lds(&s_rt);
   const BB b = unpack(root);
-  const int k = wave_legal(b, D.pr.flags, s_raw, s_sorted);
+  __syncthreads();
+  const int k = wave_legal(b, D.pr.flags, s_rt, s_l);
   if (lane == 0) {
     if (k <= 0) atomicOr(D.pr.err, k < 0 ? ERR_KMAX : ERR_ROOT);
     D.gm.root_k[g] = k;
@@ -310,11 +344,44 @@ void launch_move_begin(const Dev& d, hipStream_t s) {
 // One simulation for every active game (exp/agent.py:41-88): descend from the root by
 // PUCT until an unvisited node (expand: terminal -> back up, else queue the leaf for
 // the network) or a stored terminal (back up -terminal, the reference's sign quirk).
+#ifdef MTAZ_NET_DIAG
+// diagnostic library only: k_select phase cycles per game, summed over launches (plain adds, one
+// wave per game per launch: atomics on shared counters would themselves serialise the kernel)
+// [waves, find, select, legal, outcome, insert/init/backup, total, depth]
+constexpr int SEL_STAMP_GAMES = 65536;
+__device__ unsigned long long g_sel_cyc[SEL_STAMP_GAMES * 8];
+#define SEL_T(i)                                      \
+  {                                                   \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    sel_acc[i] += t_ - sel_t;                         \
+    sel_t = t_;                                       \
+  }
+#define SEL_FIN()                                                                        \
+  if (lane == 0 && g < SEL_STAMP_GAMES) {                                                \
+    sel_acc[6] = __builtin_amdgcn_s_memtime() - sel_t0;                                  \
+    sel_acc[0] = 1;                                                                      \
+    sel_acc[7] = depth;                                                                  \
+    for (int i_ = 0; i_ < 8; ++i_) g_sel_cyc[(size_t)g * 8 + i_] += sel_acc[i_];         \
+  }
+#else
+#define SEL_T(i)
+#define SEL_FIN()
+#endif
+
 __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
 #pragma clang fp contract(off)
-  __shared__ uint16_t s_raw[KMAX], s_sorted[KMAX];
+  __shared__ LegalLds s_l;
+  __shared__ RuleTables s_rt;
   const int g = blockIdx.x, lane = threadIdx.x;
+  if (lane == 0) D.lf.gnode[g] = NONE;
   if (!D.gm.active[g]) return;
+  load_rules_lds(&s_rt);
+  __syncthreads();
+#ifdef MTAZ_NET_DIAG
+  unsigned long long sel_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long sel_t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long sel_t = sel_t0;
+#endif
   const Trees& T = D.tr;
   const int t = 2 * g + D.gm.agent[g];
   const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
@@ -324,15 +391,18 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
   int depth = 0;
   for (;;) {
     const uint32_t n = tree_find(T, t, pos);
+    SEL_T(1);
     if (n == NONE) {
       // ---- expansion (exp/agent.py:57-73) ----
       const BB b = unpack(pos);
-      const int k = wave_legal(b, D.pr.flags, s_raw, s_sorted);
+      const int k = wave_legal(b, D.pr.flags, s_rt, s_l);
+      SEL_T(3);
       if (k < 0) {
         if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
         return;
       }
-      const int oc = outcome(b, k, in_check(b), D.pr.flags, D.pr.move_cap, 1);
+      const int oc = outcome(b, k, in_check(b, s_rt), D.pr.flags, D.pr.move_cap, 1, s_rt);
+      SEL_T(4);
       uint32_t nn = NONE, e0 = 0;
       if (lane == 0) {
         nn = tree_insert(T, t, pos, D.pr.err);
@@ -356,11 +426,8 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
               T.node_k[nbase + nn] = (uint16_t)k;
               T.node_e0[nbase + nn] = e0;
               T.node_sumN[nbase + nn] = 0;
-              const int slot = atomicAdd(D.lf.count, 1);
-              D.lf.game[slot] = g;
-              D.lf.tree[slot] = t;
-              D.lf.node[slot] = nn;
-              D.lf.pos[slot] = pos;
+              D.lf.gnode[g] = nn;
+              D.lf.gpos[g] = pos;
               D.gm.path_len[g] = depth;
             }
           }
@@ -370,16 +437,20 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
       e0 = __shfl(e0, 0, 64);
       if (oc == ONGOING && nn != NONE) {
         for (int c = lane; c < k; c += 64) {
-          T.e_code[ebase + e0 + c] = s_sorted[c];
+          T.e_code[ebase + e0 + c] = s_l.sorted[c];
           T.e_P[ebase + e0 + c] = 0.f;
           T.e_Q[ebase + e0 + c] = 0.0;
           T.e_N[ebase + e0 + c] = 0;
         }
       }
+      SEL_T(5);
+      SEL_FIN();
       return;
     }
     if (T.node_term[nbase + n]) {
       if (lane == 0) backup_path(T, t, pn, pe, depth, -T.node_tval[nbase + n]);
+      SEL_T(5);
+      SEL_FIN();
       return;
     }
     // ---- selection (exp/agent.py:79-85) ----
@@ -438,12 +509,64 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
     ++depth;
     const int code = T.e_code[ebase + e0 + a];
     pos = pack(dev_apply_code(unpack(pos), code));
+    SEL_T(2);
   }
 }
 
+// The leaf batch in game order: one workgroup, thread i scans a run of consecutive games, a block
+// scan of the run counts places each thread's leaves.
+__global__ __launch_bounds__(1024) void k_leaf_compact(Dev D) {
+  __shared__ int s_w[16];
+  const int G = D.pr.G, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (G + 1023) / 1024;
+  const int g0 = tid * per, g1 = min(G, g0 + per);
+  int c = 0;
+  for (int g = g0; g < g1; ++g) c += D.lf.gnode[g] != NONE;
+  const int incl = wave_incl_scan(c);
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  int slot = incl - c, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int x = s_w[i];
+    slot += i < w ? x : 0;
+    tot += x;
+  }
+  for (int g = g0; g < g1; ++g) {
+    const uint32_t n = D.lf.gnode[g];
+    if (n != NONE) {
+      D.lf.game[slot] = g;
+      D.lf.tree[slot] = 2 * g + D.gm.agent[g];
+      D.lf.node[slot] = n;
+      D.lf.pos[slot] = D.lf.gpos[g];
+      ++slot;
+    }
+  }
+  if (tid == 0) *D.lf.count = tot;
+}
+
+// one simulation's selection: k_select, then the dense leaf list and count
 void launch_select(const Dev& d, int sim, hipStream_t s) {
   hipLaunchKernelGGL(k_select, dim3(d.pr.G), dim3(64), 0, s, d, sim);
+  hipLaunchKernelGGL(k_leaf_compact, dim3(1), dim3(1024), 0, s, d);
 }
+
+#ifdef MTAZ_NET_DIAG
+int diag_select_stamps(unsigned long long* out8, int reset) {
+  std::vector<unsigned long long> v((size_t)SEL_STAMP_GAMES * 8);
+  if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_sel_cyc), v.size() * 8) != hipSuccess) return -1;
+  if (out8) {
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    for (size_t g = 0; g < (size_t)SEL_STAMP_GAMES; ++g)
+      for (int i = 0; i < 8; ++i) out8[i] += v[g * 8 + i];
+  }
+  if (reset) {
+    std::fill(v.begin(), v.end(), 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_cyc), v.data(), v.size() * 8) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // Leaf expansion finish + backup (exp/agent.py:68-72): store P, back up v.
 __global__ void k_backup(Dev D) {

@@ -623,6 +623,8 @@ static int engine_alloc(mtaz_engine* h) {
   HIPCHK(hipMemset(gm.outcome, 0, G * 4));
   h->noise_cap = (size_t)G * h->sims * 16;
   ECHK(h->dalloc(&gm.noise, h->noise_cap));
+  ECHK(h->dalloc(&lf.gnode, G));
+  ECHK(h->dalloc(&lf.gpos, G));
   ECHK(h->dalloc(&lf.count, 1));
   ECHK(h->dalloc(&lf.game, G));
   ECHK(h->dalloc(&lf.tree, G));
@@ -1085,6 +1087,14 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
 // 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms.  The
 // timing-only diagnostic builds (wrong results by construction) exist only in a library built
 // with MTAZ_NET_DIAG (tools/bench_net.py --diag).
+#ifdef MTAZ_NET_DIAG
+// diagnostic library only (tools/select_stamps.py): k_select phase cycle sums since the last reset
+extern "C" int mtaz_diag_select_stamps(unsigned long long* out8, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return diag_select_stamps(out8, reset);
+}
+#endif
+
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
   if (h->precision == NET_F16X3) ok = ok || variant == 1024;
@@ -1248,7 +1258,6 @@ extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t
 }
 
 static int sim_gpu(mtaz_engine* h, int sim) {
-  HIPCHK(hipMemsetAsync(h->d.lf.count, 0, 4, h->stream));
   // timing: per wave three events on the engine stream: [select begin, network begin, network end]
   hipEvent_t eb = nullptr, ee = nullptr;
   if (h->timing) {
@@ -1281,7 +1290,6 @@ extern "C" int mtaz_simulate(mtaz_engine* h, int first_sim, int n_sims) {
 
 extern "C" int mtaz_sim_select(mtaz_engine* h, int sim) {
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemsetAsync(h->d.lf.count, 0, 4, h->stream));
   launch_select(h->d, sim, h->stream);
   HIPCHK(hipGetLastError());
   return check_err(h);

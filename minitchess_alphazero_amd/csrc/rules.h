@@ -107,23 +107,25 @@ HD int lsb(uint32_t x) { return __builtin_ctz(x); }
 HD int msb(uint32_t x) { return 31 - __builtin_clz(x); }
 HD int popc(uint32_t x) { return __builtin_popcount(x); }
 
-HD uint32_t slide_pos(int d, int sq, uint32_t occ) {
-  uint32_t a = MTAZ_RT.ray[d][sq];
+// Every table lookup below goes through `RT`: the constant tables by default; device kernels
+// that generate moves pass a copy in LDS (load_rules_lds, mtaz_device.hip).
+HD uint32_t slide_pos(int d, int sq, uint32_t occ, const RuleTables& RT = MTAZ_RT) {
+  uint32_t a = RT.ray[d][sq];
   uint32_t bl = a & occ;
-  if (bl) a &= ~MTAZ_RT.ray[d][lsb(bl)];
+  if (bl) a &= ~RT.ray[d][lsb(bl)];
   return a;
 }
-HD uint32_t slide_neg(int d, int sq, uint32_t occ) {
-  uint32_t a = MTAZ_RT.ray[d][sq];
+HD uint32_t slide_neg(int d, int sq, uint32_t occ, const RuleTables& RT = MTAZ_RT) {
+  uint32_t a = RT.ray[d][sq];
   uint32_t bl = a & occ;
-  if (bl) a &= ~MTAZ_RT.ray[d][msb(bl)];
+  if (bl) a &= ~RT.ray[d][msb(bl)];
   return a;
 }
-HD uint32_t rook_att(int sq, uint32_t occ) {
-  return slide_pos(0, sq, occ) | slide_neg(1, sq, occ) | slide_pos(2, sq, occ) | slide_neg(3, sq, occ);
+HD uint32_t rook_att(int sq, uint32_t occ, const RuleTables& RT = MTAZ_RT) {
+  return slide_pos(0, sq, occ, RT) | slide_neg(1, sq, occ, RT) | slide_pos(2, sq, occ, RT) | slide_neg(3, sq, occ, RT);
 }
-HD uint32_t bishop_att(int sq, uint32_t occ) {
-  return slide_pos(4, sq, occ) | slide_pos(5, sq, occ) | slide_neg(6, sq, occ) | slide_neg(7, sq, occ);
+HD uint32_t bishop_att(int sq, uint32_t occ, const RuleTables& RT = MTAZ_RT) {
+  return slide_pos(4, sq, occ, RT) | slide_pos(5, sq, occ, RT) | slide_neg(6, sq, occ, RT) | slide_neg(7, sq, occ, RT);
 }
 
 HD int piece_type_at(const BB& b, int sq) {
@@ -138,15 +140,15 @@ HD int piece_type_at(const BB& b, int sq) {
 }
 
 // Is `sq` attacked by side `by_white`?  (oracle/rules.py is_attacked)
-HD bool attacked(const BB& b, int sq, int by_white) {
+HD bool attacked(const BB& b, int sq, int by_white, const RuleTables& RT = MTAZ_RT) {
   const uint32_t x = by_white ? b.w : b.b;
   const uint32_t occ = b.w | b.b;
-  if (MTAZ_RT.knight[sq] & b.knight & x) return true;
-  if (MTAZ_RT.king[sq] & b.king & x) return true;
+  if (RT.knight[sq] & b.knight & x) return true;
+  if (RT.king[sq] & b.king & x) return true;
   // a pawn of colour X on p attacks sq  <=>  p is attacked from sq by a pawn of the other colour
-  if (MTAZ_RT.pawn_att[by_white ? 1 : 0][sq] & b.pawn & x) return true;
-  if (rook_att(sq, occ) & (b.rook | b.queen) & x) return true;
-  if (bishop_att(sq, occ) & (b.bishop | b.queen) & x) return true;
+  if (RT.pawn_att[by_white ? 1 : 0][sq] & b.pawn & x) return true;
+  if (rook_att(sq, occ, RT) & (b.rook | b.queen) & x) return true;
+  if (bishop_att(sq, occ, RT) & (b.bishop | b.queen) & x) return true;
   return false;
 }
 
@@ -155,13 +157,13 @@ HD int king_sq(const BB& b, int white) {
   return k ? lsb(k) : -1;
 }
 
-HD bool in_check(const BB& b) {
+HD bool in_check(const BB& b, const RuleTables& RT = MTAZ_RT) {
   const int k = king_sq(b, b.white);
-  return k >= 0 && attacked(b, k, !b.white);
+  return k >= 0 && attacked(b, k, !b.white, RT);
 }
 
 // Pseudo-legal destinations of the side-to-move piece on sq (oracle pseudo_targets).
-HD uint32_t pseudo_targets(const BB& b, int sq, uint32_t flags) {
+HD uint32_t pseudo_targets(const BB& b, int sq, uint32_t flags, const RuleTables& RT = MTAZ_RT) {
   const uint32_t own = b.white ? b.w : b.b, opp = b.white ? b.b : b.w;
   const uint32_t occ = own | opp;
   const int t = piece_type_at(b, sq);
@@ -177,14 +179,14 @@ HD uint32_t pseudo_targets(const BB& b, int sq, uint32_t flags) {
           if (!((occ >> f2) & 1u)) out |= 1u << f2;
         }
       }
-      out |= MTAZ_RT.pawn_att[b.white ? 0 : 1][sq] & opp;
+      out |= RT.pawn_att[b.white ? 0 : 1][sq] & opp;
       return out;
     }
-    case KNIGHT: return MTAZ_RT.knight[sq] & ~own;
-    case KING: return MTAZ_RT.king[sq] & ~own;
-    case BISHOP: return bishop_att(sq, occ) & ~own;
-    case ROOK: return rook_att(sq, occ) & ~own;
-    case QUEEN: return (rook_att(sq, occ) | bishop_att(sq, occ)) & ~own;
+    case KNIGHT: return RT.knight[sq] & ~own;
+    case KING: return RT.king[sq] & ~own;
+    case BISHOP: return bishop_att(sq, occ, RT) & ~own;
+    case ROOK: return rook_att(sq, occ, RT) & ~own;
+    case QUEEN: return (rook_att(sq, occ, RT) | bishop_att(sq, occ, RT)) & ~own;
     default: return 0;
   }
 }
@@ -193,18 +195,17 @@ HD void clear_sq(BB& b, uint32_t m) {
   const uint32_t k = ~m;
   b.w &= k; b.b &= k; b.pawn &= k; b.knight &= k; b.bishop &= k; b.rook &= k; b.queen &= k; b.king &= k;
 }
+// selects, not a switch (which the device compiler lowers to an indexed store through scratch)
 HD void set_piece(BB& b, int sq, int type, int white) {
   const uint32_t m = 1u << sq;
-  if (white) b.w |= m; else b.b |= m;
-  switch (type) {
-    case PAWN: b.pawn |= m; break;
-    case KNIGHT: b.knight |= m; break;
-    case BISHOP: b.bishop |= m; break;
-    case ROOK: b.rook |= m; break;
-    case QUEEN: b.queen |= m; break;
-    case KING: b.king |= m; break;
-    default: break;
-  }
+  b.w |= white ? m : 0u;
+  b.b |= white ? 0u : m;
+  b.pawn |= type == PAWN ? m : 0u;
+  b.knight |= type == KNIGHT ? m : 0u;
+  b.bishop |= type == BISHOP ? m : 0u;
+  b.rook |= type == ROOK ? m : 0u;
+  b.queen |= type == QUEEN ? m : 0u;
+  b.king |= type == KING ? m : 0u;
 }
 
 // python-chess Board.push for a (from, to, promotion) move of the side to move:
@@ -229,8 +230,8 @@ HD bool is_zeroing(const BB& b, int from, int to) {
 
 // Legal destinations of the piece on sq: pseudo targets that do not leave the
 // mover's king attacked (oracle Board._gen_legal).
-HD uint32_t legal_targets(const BB& b, int sq, uint32_t flags) {
-  uint32_t ps = pseudo_targets(b, sq, flags);
+HD uint32_t legal_targets(const BB& b, int sq, uint32_t flags, const RuleTables& RT = MTAZ_RT) {
+  uint32_t ps = pseudo_targets(b, sq, flags, RT);
   if (!ps) return 0;
   const int ksq0 = king_sq(b, b.white);
   const bool is_king = (b.king >> sq) & 1u;
@@ -242,7 +243,7 @@ HD uint32_t legal_targets(const BB& b, int sq, uint32_t flags) {
     clear_sq(n, (1u << sq) | (1u << to));
     set_piece(n, to, piece_type_at(b, sq), b.white);
     const int k = is_king ? to : ksq0;
-    if (k < 0 || !attacked(n, k, !b.white)) out |= 1u << to;
+    if (k < 0 || !attacked(n, k, !b.white, RT)) out |= 1u << to;
   }
   return out;
 }
@@ -258,29 +259,32 @@ HD int move_mult(const BB& b, int from, int to, uint32_t flags) {
 }
 
 // python-chess has_insufficient_material(color) on the 5x6 board.
-HD bool side_insufficient(const BB& b, int white) {
+HD bool side_insufficient(const BB& b, int white, const RuleTables& RT = MTAZ_RT) {
   const uint32_t own = white ? b.w : b.b, opp = white ? b.b : b.w;
   if (own & (b.pawn | b.rook | b.queen)) return false;
   if (own & b.knight) return popc(own) <= 2 && !(opp & ~b.king & ~b.queen);
   if (own & b.bishop) {
-    const uint32_t dark = MTAZ_RT.dark, light = ALL_SQ & ~dark;
+    const uint32_t dark = RT.dark, light = ALL_SQ & ~dark;
     const bool same = !(b.bishop & dark) || !(b.bishop & light);
     return same && !b.pawn && !b.knight;
   }
   return true;
 }
-HD bool insufficient_material(const BB& b) { return side_insufficient(b, 1) && side_insufficient(b, 0); }
+HD bool insufficient_material(const BB& b, const RuleTables& RT = MTAZ_RT) {
+  return side_insufficient(b, 1, RT) && side_insufficient(b, 0, RT);
+}
 
 enum Outcome { ONGOING = 0, DECISIVE = 1, DRAW = 2 };
 
 // Board.result() for a board with no move history (every MCTS episode is
 // re-created from a FEN, exp/agent.py:43, so repetition can never trigger there).
 // `reps` = number of times the current position occurred (game level only; pass 1).
-HD int outcome(const BB& b, int nlegal, bool check, uint32_t flags, int move_cap, int reps) {
+HD int outcome(const BB& b, int nlegal, bool check, uint32_t flags, int move_cap, int reps,
+           const RuleTables& RT = MTAZ_RT) {
   if (nlegal == 0 && check) return DECISIVE;
   if ((flags & RF_SEVENTYFIVE) && b.half >= 150 && nlegal > 0) return DRAW;
   if ((flags & RF_FIVEFOLD) && reps >= 5) return DRAW;
-  if ((flags & RF_INSUFFICIENT) && insufficient_material(b)) return DRAW;
+  if ((flags & RF_INSUFFICIENT) && insufficient_material(b, RT)) return DRAW;
   if (nlegal == 0) return DRAW;
   if (move_cap > 0 && b.full > move_cap) return DRAW;
   return ONGOING;
@@ -289,17 +293,39 @@ HD int outcome(const BB& b, int nlegal, bool check, uint32_t flags, int move_cap
 // ---- packing ------------------------------------------------------------------------
 HD int pos_nib(const Pos& p, int s) { return (p.sq[s >> 3] >> (4 * (s & 7))) & 15; }
 
+// nibble <-> bit-plane transposes: bit i of an 8-bit mask <-> bit 4i of a word
+HD uint32_t spread8(uint32_t x) {
+  x &= 0xffu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+HD uint32_t gather8(uint32_t x) {
+  x &= 0x11111111u;
+  x = (x | (x >> 3)) & 0x03030303u;
+  x = (x | (x >> 6)) & 0x000F000Fu;
+  return (x | (x >> 12)) & 0xffu;
+}
+
+// Branch-free through bit planes of the nibbles (type bits 0..2, colour bit 3): a piece type t
+// has bit 0 for P B Q (1 3 5), bit 1 for N B K (2 3 6), bit 2 for R Q K (4 5 6).
 HD BB unpack(const Pos& p) {
-  BB b{};
+  uint32_t pl[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    uint32_t word = p.sq[w];
-    for (int j = 0; j < 8; ++j) {
-      const int s = w * 8 + j;
-      const int nib = (word >> (4 * j)) & 15;
-      if (s < NSQ && nib) set_piece(b, s, nib & 7, !(nib & 8));
-    }
-  }
+  for (int w = 0; w < 4; ++w)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pl[k] |= gather8(p.sq[w] >> k) << (8 * w);
+  const uint32_t t0 = pl[0] & ALL_SQ, t1 = pl[1] & ALL_SQ, t2 = pl[2] & ALL_SQ, blk = pl[3] & ALL_SQ;
+  BB b{};
+  b.pawn = t0 & ~t1 & ~t2;
+  b.knight = ~t0 & t1 & ~t2;
+  b.bishop = t0 & t1 & ~t2;
+  b.rook = ~t0 & ~t1 & t2;
+  b.queen = t0 & ~t1 & t2;
+  b.king = ~t0 & t1 & t2;
+  const uint32_t occ = b.pawn | b.knight | b.bishop | b.rook | b.queen | b.king;
+  b.w = occ & ~blk;
+  b.b = occ & blk;
   b.white = p.info & 1u;
   b.half = (p.info >> 8) & 0xff;
   b.full = p.info >> 16;
@@ -307,14 +333,13 @@ HD BB unpack(const Pos& p) {
 }
 
 HD Pos pack(const BB& b) {
+  const uint32_t t0 = b.pawn | b.bishop | b.queen, t1 = b.knight | b.bishop | b.king;
+  const uint32_t t2 = b.rook | b.queen | b.king, blk = b.b;
   Pos p{};
-  for (int s = 0; s < NSQ; ++s) {
-    const int t = piece_type_at(b, s);
-    if (t) {
-      const int nib = t | (((b.b >> s) & 1u) ? 8 : 0);
-      p.sq[s >> 3] |= (uint32_t)nib << (4 * (s & 7));
-    }
-  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+    p.sq[w] = spread8(t0 >> (8 * w)) | (spread8(t1 >> (8 * w)) << 1) | (spread8(t2 >> (8 * w)) << 2) |
+              (spread8(blk >> (8 * w)) << 3);
   const uint32_t half = b.half > 255 ? 255u : (uint32_t)b.half;   // saturates (> the 75-move bound)
   p.info = (b.white ? 1u : 0u) | (half << 8) | ((uint32_t)b.full << 16);
   return p;
