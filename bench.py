@@ -217,7 +217,8 @@ def main():
             dist.barrier()
 
     tot = {'sims': 0.0, 'nn_evals': 0.0, 'plies': 0.0, 'trunk_ms': 0.0, 'trunk_boards': 0.0, 'waves': 0.0,
-           'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0, 'select_ms': 0.0}
+           'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0, 'select_ms': 0.0,
+           'compact_ms': 0.0}
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -306,7 +307,10 @@ def main():
                           'frac': tot['sims'] * TREE_BYTES_PER_SIM / (tot['select_ms'] * 1e-3) / 1e9 / HBM_PEAK_GBS
                           if tot['select_ms'] > 0 else None,
                           'avg_launch_ms': tot['select_ms'] / tot['waves'] if tot['waves'] else None,
-                          'share_of_wall': tot['select_ms'] / 1e3 / dt},
+                          'share_of_wall': tot['select_ms'] / 1e3 / dt,
+                          # k_leaf_compact (the leaf list in game order, one workgroup) follows every
+                          # k_select launch; its time is outside the k_select roofline
+                          'leaf_compact_avg_ms': tot['compact_ms'] / tot['waves'] if tot['waves'] else None},
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
     }

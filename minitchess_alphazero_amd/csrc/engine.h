@@ -24,18 +24,26 @@ enum ErrBits : int32_t {
   ERR_ILLEGAL = 64, ERR_HIST = 128, ERR_HASH = 256,
 };
 
+// A node's scalars in one 16-B record (one load per level of the descent)
+struct alignas(16) NodeHdr {
+  uint32_t e0;            // tree-local first edge
+  uint32_t sumN;          // sum of child N (exact; numpy N.sum())
+  uint32_t kt;            // bits 0..15: number of children (legal list length, duplicates
+                          // kept); HDR_TERM: terminal (exp/agent.py:59-63)
+  float tval;             // stored terminal value (= -reward: -1 or -0, exact in float)
+};
+constexpr uint32_t HDR_TERM = 1u << 16;
+__host__ __device__ __forceinline__ int hdr_k(const NodeHdr& h) { return (int)(h.kt & 0xffffu); }
+__host__ __device__ __forceinline__ bool hdr_term(const NodeHdr& h) { return (h.kt & HDR_TERM) != 0; }
+
 // MCTS transposition DAG per (game, agent): exp/agent.py:29-36 keeps
 // {Q, N, P, terminal, visited, legal_moves} keyed by FEN; here a node is the
 // packed Pos key in an open-addressing table, its children a contiguous edge
-// range (SoA: code u16, P f32, Q f64, N u32).  Tree t owns nodes [t*NC, (t+1)*NC),
+// range (SoA: code u16, P f32, Q f64, N u32, child node).  Tree t owns nodes [t*NC, (t+1)*NC),
 // hash slots [t*HC, ...), edges [t*EC, ...).
 struct Trees {
   Pos* node_pos;
-  uint32_t* node_e0;      // tree-local first edge
-  uint16_t* node_k;       // number of children (legal list length, duplicates kept)
-  uint8_t* node_term;     // 1 = terminal (exp/agent.py:59-63)
-  double* node_tval;      // stored terminal value (= -reward)
-  uint32_t* node_sumN;    // sum of child N (exact; numpy N.sum())
+  NodeHdr* node_hdr;
   uint32_t* hash;         // node index + 1, 0 = empty
   uint32_t* n_nodes;      // [T]
   uint32_t* n_edges;      // [T]
@@ -43,11 +51,13 @@ struct Trees {
   float* e_P;
   double* e_Q;
   uint32_t* e_N;
+  uint32_t* e_child;      // the child's node index once the edge has been followed, else NONE
   int NC, HC, EC;
 };
 
 struct Games {
   Pos* root;              // current game position = MCTS root
+  uint32_t* root_node;    // hint: the root's node in the agent's tree (NONE = unknown; k_select checks it)
   int32_t* agent;         // tree slot (0/1) of the agent to move
   uint8_t* active;        // 1 while the game runs
   int32_t* outcome;       // game result (Outcome)
@@ -178,7 +188,9 @@ void launch_replay_put(const Pos* pos, const int32_t* k, const int64_t* e0, cons
                        uint8_t* tokens, float* clocks, float* pi, float* reward_out, hipStream_t s);
 void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s);
 void launch_move_begin(const Dev& d, hipStream_t s);
-void launch_select(const Dev& d, int sim, hipStream_t s);
+// k_select + k_leaf_compact; count_log (optional, device) receives the leaf count, ev_mid
+// (optional) is recorded between the two kernels
+void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log = nullptr, hipEvent_t ev_mid = nullptr);
 #ifdef MTAZ_NET_DIAG
 int diag_select_stamps(unsigned long long* out8, int reset);   // k_select phase cycles (diag library)
 #endif
@@ -203,8 +215,6 @@ void launch_backup(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);
 void launch_gather_leaf_codes(const Dev& d, uint16_t* codes_out, int32_t* k_out, hipStream_t s);
-void launch_tree_dump(const Dev& d, int tree, Pos* pos, uint32_t* e0, uint16_t* k, uint8_t* term, double* tval,
-                      uint32_t* sumN, hipStream_t s);
 
 // net modes
 enum NetMode { NET_LEAVES = 0, NET_FULL_LOGITS = 1 };

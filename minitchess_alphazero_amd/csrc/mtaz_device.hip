@@ -232,59 +232,63 @@ void launch_encode_batch(const Pos* pos, int n, uint8_t* tokens, float* clocks, 
 }
 
 // ---------------------------------------------------------------------------------------
-// transposition table (open addressing, linear probing; one wave owns a tree at a time)
-__device__ __forceinline__ uint32_t tree_find(const Trees& T, int t, const Pos& p) {
+// transposition table (open addressing, linear probing; one wave owns a tree at a time).
+// Returns the node, or NONE with *slot = the empty slot the probe stopped at (where
+// tree_insert puts the position: nothing else writes the table in between), or NONE with
+// *slot = HC when the table is full.
+__device__ __forceinline__ uint32_t tree_find(const Trees& T, int t, const Pos& p, uint32_t* slot) {
   const uint32_t mask = (uint32_t)T.HC - 1;
   const uint32_t* ht = T.hash + (size_t)t * T.HC;
   const Pos* np = T.node_pos + (size_t)t * T.NC;
   uint32_t h = pos_hash(p) & mask;
   for (int probe = 0; probe < T.HC; ++probe) {
     const uint32_t v = ht[h];
-    if (v == 0) return NONE;
+    if (v == 0) {
+      *slot = h;
+      return NONE;
+    }
     if (pos_eq(np[v - 1], p)) return v - 1;
     h = (h + 1) & mask;
   }
+  *slot = (uint32_t)T.HC;
   return NONE;
 }
 
-// single lane
-__device__ uint32_t tree_insert(const Trees& T, int t, const Pos& p, int32_t* err) {
-  const uint32_t n = T.n_nodes[t];
-  if (n >= (uint32_t)T.NC) {
+// single lane; `n_nodes` = the tree's node count (read at kernel start: only this wave adds nodes)
+__device__ uint32_t tree_insert(const Trees& T, int t, const Pos& p, uint32_t slot, uint32_t n_nodes, int32_t* err) {
+  if (n_nodes >= (uint32_t)T.NC) {
     atomicOr(err, ERR_NODES);
     return NONE;
   }
-  T.n_nodes[t] = n + 1;
-  T.node_pos[(size_t)t * T.NC + n] = p;
-  const uint32_t mask = (uint32_t)T.HC - 1;
-  uint32_t* ht = T.hash + (size_t)t * T.HC;
-  uint32_t h = pos_hash(p) & mask;
-  for (int probe = 0; probe < T.HC; ++probe) {
-    if (ht[h] == 0) {
-      ht[h] = n + 1;
-      return n;
-    }
-    h = (h + 1) & mask;
+  if (slot >= (uint32_t)T.HC) {
+    atomicOr(err, ERR_HASH);
+    return NONE;
   }
-  atomicOr(err, ERR_HASH);
-  return NONE;
+  T.n_nodes[t] = n_nodes + 1;
+  T.node_pos[(size_t)t * T.NC + n_nodes] = p;
+  T.hash[(size_t)t * T.HC + slot] = n_nodes + 1;
+  return n_nodes;
 }
 
-// exp/agent.py:47-52, one lane: for (node, a) in reversed(chain): value = -value;
-// Q[a] = (N[a]*Q[a] + value) / (N[a] + 1); N[a] += 1.  Exact fp64, no contraction.
-__device__ void backup_path(const Trees& T, int t, const uint32_t* pn, const uint32_t* pe, int depth, double v) {
+// exp/agent.py:47-52: for (node, a) in reversed(chain): value = -value;
+// Q[a] = (N[a]*Q[a] + value) / (N[a] + 1); N[a] += 1.  Exact fp64, no contraction.  The levels
+// are independent (level d sees (-1)^(depth - d) v, and a chain never repeats a node: the
+// fullmove number grows along it), so lane d updates level d.  Call with all lanes of a wave.
+__device__ __forceinline__ void backup_path(const Trees& T, int t, const uint32_t* pn, const uint32_t* pe, int depth,
+                                            double v, int lane) {
 #pragma clang fp contract(off)
   const size_t eb = (size_t)t * T.EC, nbase = (size_t)t * T.NC;
-  for (int d = depth - 1; d >= 0; --d) {
-    v = -v;
+  for (int d = lane; d < depth; d += 64) {
+    const double vd = ((depth - d) & 1) ? -v : v;
     const size_t e = eb + pe[d];
-    const double N = (double)T.e_N[e];
+    const uint32_t Ni = T.e_N[e];
+    const double N = (double)Ni;
     const double Q = T.e_Q[e];
     const double prod = N * Q;
-    const double num = prod + v;
+    const double num = prod + vd;
     T.e_Q[e] = num / (N + 1.0);
-    T.e_N[e] += 1;
-    T.node_sumN[nbase + pn[d]] += 1;
+    T.e_N[e] = Ni + 1;
+    T.node_hdr[nbase + pn[d]].sumN += 1;
   }
 }
 
@@ -307,6 +311,7 @@ void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStrea
 
 // Move start: does the agent's table already hold the root (exp/agent.py:57)?  The host
 // needs k and "root is new" to draw exactly sims - root_new Dirichlet vectors (:81-82).
+// Also leaves the root's node index as k_select's hint (Games::root_node).
 __global__ __launch_bounds__(64) void k_move_begin(Dev D) {
   __shared__ LegalLds s_l;
   __shared__ RuleTables s_rt;
@@ -317,11 +322,14 @@ __global__ __launch_bounds__(64) void k_move_begin(Dev D) {
   }
   const int t = 2 * g + D.gm.agent[g];
   const Pos root = D.gm.root[g];
-  const uint32_t n = tree_find(D.tr, t, root);
+  uint32_t slot;
+  const uint32_t n = tree_find(D.tr, t, root, &slot);
+  if (lane == 0) D.gm.root_node[g] = n;
   if (n != NONE) {
     if (lane == 0) {
-      if (D.tr.node_term[(size_t)t * D.tr.NC + n]) atomicOr(D.pr.err, ERR_ROOT);
-      D.gm.root_k[g] = D.tr.node_k[(size_t)t * D.tr.NC + n];
+      const NodeHdr hd = D.tr.node_hdr[(size_t)t * D.tr.NC + n];
+      if (hdr_term(hd)) atomicOr(D.pr.err, ERR_ROOT);
+      D.gm.root_k[g] = hdr_k(hd);
       D.gm.root_new[g] = 0;
     }
     return;
@@ -344,6 +352,12 @@ void launch_move_begin(const Dev& d, hipStream_t s) {
 // One simulation for every active game (exp/agent.py:41-88): descend from the root by
 // PUCT until an unvisited node (expand: terminal -> back up, else queue the leaf for
 // the network) or a stored terminal (back up -terminal, the reference's sign quirk).
+// The descent follows node indices, not hash lookups: the root's from Games::root_node
+// (checked against the node's stored position and the tree's node count, so a stale hint
+// only costs a lookup), a child's from its edge (Trees::e_child, filled the first time the
+// edge is followed).  The position is still carried along (the leaf's network input, the
+// lookup of a child not yet linked).  Per level: one node-header load, then one pass over
+// the children's P, Q, N, code and child index.
 #ifdef MTAZ_NET_DIAG
 // diagnostic library only: k_select phase cycles per game, summed over launches (plain adds, one
 // wave per game per launch: atomics on shared counters would themselves serialise the kernel)
@@ -375,88 +389,104 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
   const int g = blockIdx.x, lane = threadIdx.x;
   if (lane == 0) D.lf.gnode[g] = NONE;
   if (!D.gm.active[g]) return;
-  load_rules_lds(&s_rt);
-  __syncthreads();
 #ifdef MTAZ_NET_DIAG
   unsigned long long sel_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long sel_t0 = __builtin_amdgcn_s_memtime();
   unsigned long long sel_t = sel_t0;
 #endif
+  load_rules_lds(&s_rt);
   const Trees& T = D.tr;
   const int t = 2 * g + D.gm.agent[g];
   const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
   uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
+  const uint32_t n_nodes = T.n_nodes[t], n_edges = T.n_edges[t];
   Pos pos = D.gm.root[g];
   int depth = 0;
+  uint32_t n = D.gm.root_node[g];
+  // the hinted node's position and header in one round trip (the header is used only if the
+  // position matches)
+  const size_t nh = nbase + (n < (uint32_t)T.NC ? n : 0u);
+  const Pos hpos = T.node_pos[nh];
+  NodeHdr hd_pre = T.node_hdr[nh];
+  if (n >= n_nodes || !pos_eq(hpos, pos)) n = NONE;
+  bool linked = n != NONE;      // n is pos's node, known without a lookup
+  bool pre = linked;            // hd_pre is n's header
+  uint32_t pedge = NONE;        // the edge that led here (tree-local), NONE at the root
+  __syncthreads();
   for (;;) {
-    const uint32_t n = tree_find(T, t, pos);
-    SEL_T(1);
-    if (n == NONE) {
-      // ---- expansion (exp/agent.py:57-73) ----
-      const BB b = unpack(pos);
-      const int k = wave_legal(b, D.pr.flags, s_rt, s_l);
-      SEL_T(3);
-      if (k < 0) {
-        if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
-        return;
-      }
-      const int oc = outcome(b, k, in_check(b, s_rt), D.pr.flags, D.pr.move_cap, 1, s_rt);
-      SEL_T(4);
-      uint32_t nn = NONE, e0 = 0;
-      if (lane == 0) {
-        nn = tree_insert(T, t, pos, D.pr.err);
-        if (nn != NONE) {
-          if (oc != ONGOING) {
-            const double value = (oc == DECISIVE) ? -1.0 : -0.0;   // -reward
-            T.node_term[nbase + nn] = 1;
-            T.node_tval[nbase + nn] = value;
-            T.node_k[nbase + nn] = 0;
-            T.node_e0[nbase + nn] = 0;
-            T.node_sumN[nbase + nn] = 0;
-            backup_path(T, t, pn, pe, depth, value);
-          } else {
-            e0 = T.n_edges[t];
-            if (e0 + (uint32_t)k > (uint32_t)T.EC) {
-              atomicOr(D.pr.err, ERR_EDGES);
-              nn = NONE;
+    if (!linked) {
+      uint32_t slot;
+      n = tree_find(T, t, pos, &slot);
+      SEL_T(1);
+      if (n == NONE) {
+        // ---- expansion (exp/agent.py:57-73) ----
+        const BB b = unpack(pos);
+        const int k = wave_legal(b, D.pr.flags, s_rt, s_l);
+        SEL_T(3);
+        if (k < 0) {
+          if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
+          return;
+        }
+        const int oc = outcome(b, k, in_check(b, s_rt), D.pr.flags, D.pr.move_cap, 1, s_rt);
+        SEL_T(4);
+        uint32_t nn = NONE;
+        if (lane == 0) {
+          nn = tree_insert(T, t, pos, slot, n_nodes, D.pr.err);
+          if (nn != NONE && oc == ONGOING && n_edges + (uint32_t)k > (uint32_t)T.EC) {
+            atomicOr(D.pr.err, ERR_EDGES);
+            nn = NONE;
+          }
+          if (nn != NONE) {
+            if (oc != ONGOING) {
+              T.node_hdr[nbase + nn] = NodeHdr{0u, 0u, HDR_TERM, (oc == DECISIVE) ? -1.0f : -0.0f};   // -reward
             } else {
-              T.n_edges[t] = e0 + k;
-              T.node_term[nbase + nn] = 0;
-              T.node_k[nbase + nn] = (uint16_t)k;
-              T.node_e0[nbase + nn] = e0;
-              T.node_sumN[nbase + nn] = 0;
+              T.n_edges[t] = n_edges + k;
+              T.node_hdr[nbase + nn] = NodeHdr{n_edges, 0u, (uint32_t)k, 0.0f};
               D.lf.gnode[g] = nn;
               D.lf.gpos[g] = pos;
               D.gm.path_len[g] = depth;
             }
+            if (pedge != NONE) T.e_child[ebase + pedge] = nn;
+            else D.gm.root_node[g] = nn;
           }
         }
-      }
-      nn = __shfl(nn, 0, 64);
-      e0 = __shfl(e0, 0, 64);
-      if (oc == ONGOING && nn != NONE) {
-        for (int c = lane; c < k; c += 64) {
-          T.e_code[ebase + e0 + c] = s_l.sorted[c];
-          T.e_P[ebase + e0 + c] = 0.f;
-          T.e_Q[ebase + e0 + c] = 0.0;
-          T.e_N[ebase + e0 + c] = 0;
+        nn = __shfl(nn, 0, 64);
+        if (nn != NONE) {
+          if (oc == ONGOING) {
+            for (int c = lane; c < k; c += 64) {
+              T.e_code[ebase + n_edges + c] = s_l.sorted[c];
+              T.e_P[ebase + n_edges + c] = 0.f;
+              T.e_Q[ebase + n_edges + c] = 0.0;
+              T.e_N[ebase + n_edges + c] = 0;
+              T.e_child[ebase + n_edges + c] = NONE;
+            }
+          } else {
+            backup_path(T, t, pn, pe, depth, (oc == DECISIVE) ? -1.0 : -0.0, lane);
+          }
         }
+        SEL_T(5);
+        SEL_FIN();
+        return;
       }
-      SEL_T(5);
-      SEL_FIN();
-      return;
+      // found by lookup (a transposition, or the root without a valid hint): link it
+      if (lane == 0) {
+        if (pedge != NONE) T.e_child[ebase + pedge] = n;
+        else D.gm.root_node[g] = n;
+      }
     }
-    if (T.node_term[nbase + n]) {
-      if (lane == 0) backup_path(T, t, pn, pe, depth, -T.node_tval[nbase + n]);
+    const NodeHdr hd = pre ? hd_pre : T.node_hdr[nbase + n];
+    pre = false;
+    if (hdr_term(hd)) {
+      backup_path(T, t, pn, pe, depth, -(double)hd.tval, lane);
       SEL_T(5);
       SEL_FIN();
       return;
     }
     // ---- selection (exp/agent.py:79-85) ----
-    const uint32_t e0 = T.node_e0[nbase + n];
-    const int k = T.node_k[nbase + n];
-    const uint32_t S = T.node_sumN[nbase + n];
+    const uint32_t e0 = hd.e0;
+    const int k = hdr_k(hd);
+    const uint32_t S = hd.sumN;
     if (S >= (uint32_t)D.pr.sqrt_n) {
       if (lane == 0) atomicOr(D.pr.err, ERR_SQRT);
       return;
@@ -470,11 +500,14 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
     }
     double best_u = -__builtin_inf();
     int best_i = 0x7fffffff;
+    uint32_t best_cc = 0;   // winner's code | linked child (the child index in a second word)
+    uint32_t best_ch = NONE;
     for (int c = lane; c < k; c += 64) {
       const size_t e = ebase + e0 + c;
       const float Pf = T.e_P[e];
       const double Q = T.e_Q[e];
       const double N = (double)T.e_N[e];
+      const uint32_t code = T.e_code[e], child = T.e_child[e];
       double tt;
       if (root) {
         // P = 0.75*P (float32) + 0.25*dirichlet (float64)  -> float64
@@ -489,13 +522,14 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
         tt = (double)(cp * (float)sq);            // numpy 1.x: stays float32
       }
       const double u = Q + tt / (1.0 + N);
-      if (u > best_u) { best_u = u; best_i = c; }
+      if (u > best_u) { best_u = u; best_i = c; best_cc = code; best_ch = child; }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       const double ou = __shfl_xor(best_u, o, 64);
       const int oi = __shfl_xor(best_i, o, 64);
-      if (ou > best_u || (ou == best_u && oi < best_i)) { best_u = ou; best_i = oi; }
+      const uint32_t occ = __shfl_xor(best_cc, o, 64), och = __shfl_xor(best_ch, o, 64);
+      if (ou > best_u || (ou == best_u && oi < best_i)) { best_u = ou; best_i = oi; best_cc = occ; best_ch = och; }
     }
     const int a = best_i;
     if (depth >= D.gm.DMAX) {
@@ -507,48 +541,73 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
       pe[depth] = e0 + a;
     }
     ++depth;
-    const int code = T.e_code[ebase + e0 + a];
-    pos = pack(dev_apply_code(unpack(pos), code));
+    pedge = e0 + a;
+    pos = pack(dev_apply_code(unpack(pos), (int)best_cc));
+    n = best_ch;
+    linked = n != NONE;
     SEL_T(2);
   }
 }
 
-// The leaf batch in game order: one workgroup, thread i scans a run of consecutive games, a block
-// scan of the run counts places each thread's leaves.
-__global__ __launch_bounds__(1024) void k_leaf_compact(Dev D) {
+// The leaf batch in game order: one workgroup; per chunk of 4,096 games thread i holds games
+// 4i..4i+3 in registers (their leaf, agent and position in one round of loads: loads placed after
+// the stores would wait for them), a block scan of the per-thread counts places its leaves.
+// Also logs the count (count_log, when given).
+__global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restrict__ count_log) {
+  constexpr int PER = 4;
   __shared__ int s_w[16];
   const int G = D.pr.G, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int per = (G + 1023) / 1024;
-  const int g0 = tid * per, g1 = min(G, g0 + per);
-  int c = 0;
-  for (int g = g0; g < g1; ++g) c += D.lf.gnode[g] != NONE;
-  const int incl = wave_incl_scan(c);
-  if (lane == 63) s_w[w] = incl;
-  __syncthreads();
-  int slot = incl - c, tot = 0;
+  int base = 0;
+  for (int c0 = 0; c0 < G; c0 += 1024 * PER) {
+    const int g0 = c0 + tid * PER;
+    uint32_t nd[PER];
+    int ag[PER];
+    Pos ps[PER];
+    int c = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int x = s_w[i];
-    slot += i < w ? x : 0;
-    tot += x;
-  }
-  for (int g = g0; g < g1; ++g) {
-    const uint32_t n = D.lf.gnode[g];
-    if (n != NONE) {
-      D.lf.game[slot] = g;
-      D.lf.tree[slot] = 2 * g + D.gm.agent[g];
-      D.lf.node[slot] = n;
-      D.lf.pos[slot] = D.lf.gpos[g];
-      ++slot;
+    for (int j = 0; j < PER; ++j) {
+      const bool in = g0 + j < G;
+      nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
+      ag[j] = in ? D.gm.agent[g0 + j] : 0;
+      ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
     }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) c += nd[j] != NONE;
+    const int incl = wave_incl_scan(c);
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    int slot = base + incl - c, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int x = s_w[i];
+      slot += i < w ? x : 0;
+      tot += x;
+    }
+    __syncthreads();   // s_w is rewritten by the next chunk
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (nd[j] != NONE) {
+        const int g = g0 + j;
+        D.lf.game[slot] = g;
+        D.lf.tree[slot] = 2 * g + ag[j];
+        D.lf.node[slot] = nd[j];
+        D.lf.pos[slot] = ps[j];
+        ++slot;
+      }
+    }
+    base += tot;
   }
-  if (tid == 0) *D.lf.count = tot;
+  if (tid == 0) {
+    *D.lf.count = base;
+    if (count_log) *count_log = base;
+  }
 }
 
 // one simulation's selection: k_select, then the dense leaf list and count
-void launch_select(const Dev& d, int sim, hipStream_t s) {
+void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log, hipEvent_t ev_mid) {
   hipLaunchKernelGGL(k_select, dim3(d.pr.G), dim3(64), 0, s, d, sim);
-  hipLaunchKernelGGL(k_leaf_compact, dim3(1), dim3(1024), 0, s, d);
+  if (ev_mid) (void)hipEventRecord(ev_mid, s);
+  hipLaunchKernelGGL(k_leaf_compact, dim3(1), dim3(1024), 0, s, d, count_log);
 }
 
 #ifdef MTAZ_NET_DIAG
@@ -568,24 +627,25 @@ int diag_select_stamps(unsigned long long* out8, int reset) {
 }
 #endif
 
-// Leaf expansion finish + backup (exp/agent.py:68-72): store P, back up v.
-__global__ void k_backup(Dev D) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Leaf expansion finish + backup (exp/agent.py:68-72): store P, back up v.  One wave per leaf:
+// lanes copy the priors and update one path level each.
+__global__ __launch_bounds__(256) void k_backup(Dev D) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= *D.lf.count) return;
   const Trees& T = D.tr;
   const int g = D.lf.game[i], t = D.lf.tree[i];
   const uint32_t n = D.lf.node[i];
   const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
-  const int k = T.node_k[nbase + n];
-  const uint32_t e0 = T.node_e0[nbase + n];
-  for (int c = 0; c < k; ++c) T.e_P[ebase + e0 + c] = D.lf.P[(size_t)i * KMAX + c];
+  const NodeHdr hd = T.node_hdr[nbase + n];
+  const int k = hdr_k(hd);
+  for (int c = lane; c < k; c += 64) T.e_P[ebase + hd.e0 + c] = D.lf.P[(size_t)i * KMAX + c];
   const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
-  backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i]);
+  backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i], lane);
 }
 
 void launch_backup(const Dev& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_backup, dim3((d.pr.G + 63) / 64), dim3(64), 0, s, d);
+  hipLaunchKernelGGL(k_backup, dim3((d.pr.G + 3) / 4), dim3(256), 0, s, d);
 }
 
 __global__ void k_gather_leaf_codes(Dev D, uint16_t* __restrict__ codes, int32_t* __restrict__ kout) {
@@ -594,8 +654,9 @@ __global__ void k_gather_leaf_codes(Dev D, uint16_t* __restrict__ codes, int32_t
   const Trees& T = D.tr;
   const int t = D.lf.tree[i];
   const uint32_t n = D.lf.node[i];
-  const int k = T.node_k[(size_t)t * T.NC + n];
-  const uint32_t e0 = T.node_e0[(size_t)t * T.NC + n];
+  const NodeHdr hd = T.node_hdr[(size_t)t * T.NC + n];
+  const int k = hdr_k(hd);
+  const uint32_t e0 = hd.e0;
   for (int c = threadIdx.x; c < k; c += blockDim.x) codes[(size_t)i * KMAX + c] = T.e_code[(size_t)t * T.EC + e0 + c];
   if (threadIdx.x == 0) kout[i] = k;
 }
@@ -610,13 +671,15 @@ __global__ __launch_bounds__(64) void k_move_end(Dev D, uint16_t* __restrict__ c
   if (!D.gm.active[g]) return;
   const Trees& T = D.tr;
   const int t = 2 * g + D.gm.agent[g];
-  const uint32_t n = tree_find(T, t, D.gm.root[g]);
+  uint32_t slot;
+  const uint32_t n = tree_find(T, t, D.gm.root[g], &slot);
   if (n == NONE) {
     if (lane == 0) atomicOr(D.pr.err, ERR_ROOT);
     return;
   }
-  const int k = T.node_k[(size_t)t * T.NC + n];
-  const uint32_t e0 = T.node_e0[(size_t)t * T.NC + n];
+  const NodeHdr hd = T.node_hdr[(size_t)t * T.NC + n];
+  const int k = hdr_k(hd);
+  const uint32_t e0 = hd.e0;
   if (k > kout) {
     if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
     return;
@@ -872,13 +935,13 @@ __global__ __launch_bounds__(256) void k_heads(Dev D, NetWeights W, const float*
   if (mode == NET_LEAVES && tid == 0) {
     const int t = D.lf.tree[b];
     const uint32_t n = D.lf.node[b];
-    sk = D.tr.node_k[(size_t)t * D.tr.NC + n];
+    sk = hdr_k(D.tr.node_hdr[(size_t)t * D.tr.NC + n]);
   }
   __syncthreads();
   if (mode == NET_LEAVES) {
     const int t = D.lf.tree[b];
     const uint32_t n = D.lf.node[b];
-    const uint32_t e0 = D.tr.node_e0[(size_t)t * D.tr.NC + n];
+    const uint32_t e0 = D.tr.node_hdr[(size_t)t * D.tr.NC + n].e0;
     for (int c = tid; c < sk; c += 256) scode[c] = D.tr.e_code[(size_t)t * D.tr.EC + e0 + c];
   }
   if (tid < 90) {

@@ -440,7 +440,7 @@ struct PlyRec {
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
-  ST_NODE_CAP, ST_EDGE_CAP, ST_COUNT
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_COUNT
 };
 
 template <class F>
@@ -589,11 +589,7 @@ static int engine_alloc(mtaz_engine* h) {
   gm.HMAX = 2 * max_moves + 8;
   const size_t TN = (size_t)T * tr.NC, TE = (size_t)T * tr.EC;
   ECHK(h->dalloc(&tr.node_pos, TN));
-  ECHK(h->dalloc(&tr.node_e0, TN));
-  ECHK(h->dalloc(&tr.node_k, TN));
-  ECHK(h->dalloc(&tr.node_term, TN));
-  ECHK(h->dalloc(&tr.node_tval, TN));
-  ECHK(h->dalloc(&tr.node_sumN, TN));
+  ECHK(h->dalloc(&tr.node_hdr, TN));
   ECHK(h->dalloc(&tr.hash, (size_t)T * tr.HC));
   ECHK(h->dalloc(&tr.n_nodes, T));
   ECHK(h->dalloc(&tr.n_edges, T));
@@ -601,10 +597,13 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&tr.e_P, TE));
   ECHK(h->dalloc(&tr.e_Q, TE));
   ECHK(h->dalloc(&tr.e_N, TE));
+  ECHK(h->dalloc(&tr.e_child, TE));
   HIPCHK(hipMemset(tr.hash, 0, (size_t)T * tr.HC * 4));
   HIPCHK(hipMemset(tr.n_nodes, 0, T * 4));
   HIPCHK(hipMemset(tr.n_edges, 0, T * 4));
   ECHK(h->dalloc(&gm.root, G));
+  ECHK(h->dalloc(&gm.root_node, G));
+  HIPCHK(hipMemset(gm.root_node, 0xff, G * 4));
   ECHK(h->dalloc(&gm.agent, G));
   ECHK(h->dalloc(&gm.active, G));
   ECHK(h->dalloc(&gm.outcome, G));
@@ -1258,24 +1257,24 @@ extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t
 }
 
 static int sim_gpu(mtaz_engine* h, int sim) {
-  // timing: per wave three events on the engine stream: [select begin, network begin, network end]
-  hipEvent_t eb = nullptr, ee = nullptr;
+  // timing: per wave four events on the engine stream: [select begin, leaf compaction begin,
+  // network begin, network end]
+  hipEvent_t em = nullptr, eb = nullptr, ee = nullptr;
   if (h->timing) {
-    const size_t need = 3 * (size_t)(h->wave + 1);
+    const size_t need = 4 * (size_t)(h->wave + 1);
     while (h->ev.size() < need) {
       hipEvent_t e;
       HIPCHK(hipEventCreate(&e));
       h->ev.push_back(e);
     }
-    HIPCHK(hipEventRecord(h->ev[3 * h->wave], h->stream));
-    eb = h->ev[3 * h->wave + 1];
-    ee = h->ev[3 * h->wave + 2];
+    HIPCHK(hipEventRecord(h->ev[4 * h->wave], h->stream));
+    em = h->ev[4 * h->wave + 1];
+    eb = h->ev[4 * h->wave + 2];
+    ee = h->ev[4 * h->wave + 3];
   }
-  launch_select(h->d, sim, h->stream);
+  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + h->wave : nullptr, em);
   launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, eb, ee);
   launch_backup(h->d, h->stream);
-  if (h->wave < h->count_log_cap)
-    HIPCHK(hipMemcpyAsync(h->d_count_log + h->wave, h->d.lf.count, 4, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(hipGetLastError());
   ++h->wave;
   return 0;
@@ -1385,10 +1384,14 @@ extern "C" int mtaz_tree_get(mtaz_engine* h, int tree, uint32_t* pos, uint32_t* 
   const Trees& T = h->d.tr;
   const size_t nb = (size_t)tree * T.NC, eb = (size_t)tree * T.EC;
   HIPCHK(hipMemcpy(pos, T.node_pos + nb, nn * sizeof(Pos), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(e0, T.node_e0 + nb, nn * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(k, T.node_k + nb, nn * 2, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(term, T.node_term + nb, nn, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(tval, T.node_tval + nb, nn * 8, hipMemcpyDeviceToHost));
+  std::vector<NodeHdr> hd(nn);
+  HIPCHK(hipMemcpy(hd.data(), T.node_hdr + nb, nn * sizeof(NodeHdr), hipMemcpyDeviceToHost));
+  for (int i = 0; i < nn; ++i) {
+    e0[i] = hd[i].e0;
+    k[i] = (uint16_t)hdr_k(hd[i]);
+    term[i] = hdr_term(hd[i]) ? 1 : 0;
+    tval[i] = (double)hd[i].tval;
+  }
   HIPCHK(hipMemcpy(codes, T.e_code + eb, ne * 2, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(P, T.e_P + eb, ne * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(Q, T.e_Q + eb, ne * 8, hipMemcpyDeviceToHost));
@@ -1623,14 +1626,16 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     HIPCHK(hipMemcpy(counts.data(), h->d_count_log, counts.size() * 4, hipMemcpyDeviceToHost));
   double evals = 0;
   for (int c : counts) evals += c;
-  double trunk_ms = 0, trunk_boards = 0, select_ms = 0;
+  double trunk_ms = 0, trunk_boards = 0, select_ms = 0, compact_ms = 0;
   if (h->timing) {
     for (int wv = 0; wv < h->wave && wv < (int)counts.size(); ++wv) {
-      float ms = 0, sms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, h->ev[3 * wv + 1], h->ev[3 * wv + 2]));
-      HIPCHK(hipEventElapsedTime(&sms, h->ev[3 * wv], h->ev[3 * wv + 1]));
+      float ms = 0, sms = 0, cms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, h->ev[4 * wv + 2], h->ev[4 * wv + 3]));
+      HIPCHK(hipEventElapsedTime(&sms, h->ev[4 * wv], h->ev[4 * wv + 1]));
+      HIPCHK(hipEventElapsedTime(&cms, h->ev[4 * wv + 1], h->ev[4 * wv + 2]));
       trunk_ms += ms;
       select_ms += sms;
+      compact_ms += cms;
       trunk_boards += counts[wv];
     }
   }
@@ -1664,6 +1669,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_SYNC_MS] = sync_ms;
   h->stats[ST_NET_PREC] = h->precision;
   h->stats[ST_SELECT_MS] = select_ms;
+  h->stats[ST_COMPACT_MS] = compact_ms;
   return 0;
 }
 

@@ -206,8 +206,9 @@ __device__ __forceinline__ void heads_out(const Dev& D, char* smem, int b0, int 
   if (lane == 0) D.lf.v[b] = v;
   const int t = D.lf.tree[b];
   const uint32_t n = D.lf.node[b];
-  const int k = D.tr.node_k[(size_t)t * D.tr.NC + n];
-  const uint32_t e0 = D.tr.node_e0[(size_t)t * D.tr.NC + n];
+  const NodeHdr hd = D.tr.node_hdr[(size_t)t * D.tr.NC + n];
+  const int k = hdr_k(hd);
+  const uint32_t e0 = hd.e0;
   const uint16_t* codes = D.tr.e_code + (size_t)t * D.tr.EC + e0;
   float lg[KMAX / 64];
   float mx = -__builtin_inff();
