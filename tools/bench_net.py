@@ -68,6 +68,18 @@ def main():
             res[v]['cycles'].append(float(st[:, 4].mean()))
             res[v]['ghz'].append(float((st[:, 4] / (st[:, 5] * 10.0)).mean()))   # cycles / (ticks * 10 ns) -> GHz
             res[v]['shares'].append((st[:, :4] / st[:, :4].sum(axis=1, keepdims=True)).mean(axis=0))
+    # outputs vs the first variant (64 games' engine evaluates 64 positions at a time)
+    ref = None
+    check = {}
+    for v in variants:
+        prec, var = v.split(':')
+        eng.set_precision(prec)
+        _lib.check(eng.L.mtaz_set_net_variant(eng.h, int(var)))
+        lg, vl = eng.evaluate(pos[:64])
+        if ref is None:
+            ref = (lg, vl)
+        check[v] = {'bitwise_equal_to_first': bool(np.array_equal(lg, ref[0]) and np.array_equal(vl, ref[1])),
+                    'max_logit_diff': float(np.abs(lg - ref[0]).max()), 'max_value_diff': float(np.abs(vl - ref[1]).max())}
     for v in variants:
         r = res[v]
         ms = float(np.median(r['ms']))
@@ -75,7 +87,8 @@ def main():
                'tflops_algorithmic': FLOP_PER_EVAL * args.n / (ms * 1e-3) / 1e12,
                'wg_cycles': float(np.median(r['cycles'])), 'clock_ghz_stamped': float(np.median(r['ghz'])),
                'shares': dict(zip(['stem', 'conv_kloop', 'conv_epilogue', 'heads'],
-                                  np.mean(r['shares'], axis=0).round(4).tolist()))}
+                                  np.mean(r['shares'], axis=0).round(4).tolist())),
+               'check': check[v]}
         print(json.dumps(out), flush=True)
 
 
