@@ -1,0 +1,46 @@
+"""GPU: BASELINE config 5 (self-play -> learner -> weights) across ranks, world size 2.
+
+Two ranks started as bench.py --gpus N starts them (minitchess_alphazero_amd.launch), both on cuda:0
+of the one-GPU box, gloo for the exchange (records gathered to rank 0, one flat weight broadcast).
+Games shard by global id, so two ranks of G games play exactly the games one process plays with 2G,
+the learner on rank 0 sees the same rows in the same order, and under deterministic algorithms the
+two runs must end with bitwise-identical weights after every iteration's broadcast."""
+import json
+import os
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def test_loop_two_ranks_equal_one_process(tmp_path):
+    import torch
+    from minitchess_alphazero_amd.launch import spawn_ranks
+    from minitchess_alphazero_amd.loop import flat_weights, run_loop
+    G, sims, iters = 8, 8, 2
+    out = str(tmp_path / 'loop.json')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    rc = spawn_ranks(2, [sys.executable, os.path.join(REPO, 'tests', 'rank_worker_loop.py'), out, str(G), str(sims),
+                         str(iters)], env=env)
+    assert rc == 0
+    res = json.load(open(out))
+    prev = (torch.are_deterministic_algorithms_enabled(), torch.backends.cudnn.deterministic,
+            torch.backends.cudnn.benchmark)
+    torch.use_deterministic_algorithms(True)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        hist, net = run_loop(iters, 2 * G, sims, batch_size=16, dist=None, device=0, seed=0, log=lambda s: None)
+    finally:
+        torch.use_deterministic_algorithms(prev[0])
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev[1], prev[2]
+    flat, _ = flat_weights(net, 'cpu')
+    assert len(res['history']) == iters
+    for a, b in zip(res['history'], hist):
+        assert a['games'] == b['games'] == 2 * G
+        assert a['rows'] == b['rows']          # (weights_version is a timestamp, app/base.py)
+        assert a['loss'] == b['loss'], (a['loss'], b['loss'])
+    assert res['head'] == flat[:2000].tolist() and res['tail'] == flat[-2000:].tolist()
+    assert res['sum'] == flat.double().sum().item()
