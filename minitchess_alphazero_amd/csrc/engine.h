@@ -148,7 +148,7 @@ struct NetWeights {
   // k_net_z (f16 + e4m3 cross terms): the split weights' hi and lo parts of convy, each scaled by
   // a per-layer power of two and rounded to OCP e4m3, as the A operand of
   // v_mfma_scale_f32_16x16x128_f8f6f4: [L 18][cotile 16][tap 9][chunk 2][part hi/lo][half 2]
-  // [lane 64][16 B]; lane l holds W[co = 16*cotile + (l&15)][ci = 128*chunk + 32*(l>>4) + j]
+  // [lane 64][16 B]; lane l holds W[co = zrow_co(cotile, l&15)][ci = 128*chunk + 32*(l>>4) + j]
   // (j = 16*half + byte) of that tap.  conv8_sc[2L + part] = the e8m0 scale that undoes the
   // part's power of two (127 - a).
   const uint4* conv8;
@@ -156,12 +156,18 @@ struct NetWeights {
   // k_net_z VAR 8192 (cross terms in e2m3 = fp6): the same hi / lo parts as conv8, each block of
   // 32 K (one output channel, tap, 32 input channels) in e2m3 with its own e8m0 scale:
   // [L 18][cotile 16][group 36 = (tap, chunk, part)][112 x 16 B]; per group and lane l
-  // (co = 16*cotile + (l&15), channels 128*chunk + 32*(l>>4) + perm(q)): bytes 0..15 of the 24-B
+  // (co = zrow_co(cotile, l&15), channels 128*chunk + 32*(l>>4) + q): bytes 0..15 of the 24-B
   // fp6 vector at 16 B x l, bytes 16..23 at 1024 + 8 l, the scale (u32, byte 0) at 1536 + 4 l.
-  // Value q of the vector (bits 6q..6q+5) is channel perm(q) = 16*((q>>2)&1) + 4*(q>>3) + (q&3)
-  // of the 32-channel block: the order in which the epilogue's lanes hold them.
+  // Value q of the vector (bits 6q..6q+5) is channel q of the 32-channel block.
   const uint4* conv6;
+  // k_net_z's copies of convy and stemy (both parts) with the output channels of each pair of
+  // 16-row tiles interleaved, and conv8 / conv6 in the same row order: row r of tile T is
+  // channel zrow_co(T, r), so that the epilogue's lane g holds 8 consecutive channels of a tile pair
+  // (one 16-B f16 store and two 8-B e4m3 stores per square)
+  const uint4* convz;
+  const uint4* stemz;
 };
+__host__ __device__ __forceinline__ int zrow_co(int T, int r) { return 32 * (T >> 1) + 8 * (r >> 2) + 4 * (T & 1) + (r & 3); }
 constexpr int CONV_LAYERS = 18;
 constexpr size_t CONV_W_FLOATS = (size_t)8 * 288 * 64 * 4;   // 589,824 = 256*2304
 constexpr size_t CONVX_U4_PER_LAYER = (size_t)16 * 72 * 2 * 64;  // 147,456 x 16 B = 2.36 MB (convy)

@@ -925,7 +925,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             for (int half = 0; half < 2; ++half)
               for (int lane = 0; lane < 64; ++lane)
                 for (int byte = 0; byte < 16; ++byte) {
-                  const int co = 16 * ct + (lane & 15), ci = 128 * c + 32 * (lane >> 4) + 16 * half + byte;
+                  const int co = zrow_co(ct, lane & 15), ci = 128 * c + 32 * (lane >> 4) + 16 * half + byte;
                   const size_t u4 = (((((size_t)ct * 9 + t) * 2 + c) * 2 + part) * 2 + half) * 64 + lane;
                   dst[u4 * 16 + byte] = to_e4m3(ldexp(at(part, co, t * 256 + ci), a[part]));
                 }
@@ -946,10 +946,10 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
           for (int part = 0; part < 2; ++part) {
             uint8_t* gb = dst + ((((size_t)ct * 9 + t) * 2 + c) * 2 + part) * 112 * 16;
             for (int lane = 0; lane < 64; ++lane) {
-              const int co = 16 * ct + (lane & 15);
+              const int co = zrow_co(ct, lane & 15);
               double v[32], mx = 0;
               for (int q = 0; q < 32; ++q) {
-                const int ci = 128 * c + 32 * (lane >> 4) + 16 * ((q >> 2) & 1) + 4 * (q >> 3) + (q & 3);
+                const int ci = 128 * c + 32 * (lane >> 4) + q;
                 v[q] = at(part, co, t * 256 + ci);
                 mx = std::max(mx, fabs(v[q]));
               }
@@ -971,6 +971,30 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             }
           }
   }
+  // k_net_z's row-interleaved copies of wy and sy (NetWeights::convz, stemz)
+  std::vector<_Float16> wz(wy.size()), sz(sy.size());
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const _Float16* src = wy.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    _Float16* dst = wz.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    for (int T = 0; T < 16; ++T)
+      for (int kb = 0; kb < 72; ++kb)
+        for (int part = 0; part < 2; ++part)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int c = zrow_co(T, lane & 15);
+            const size_t si = ((((size_t)(c >> 4) * 72 + kb) * 2 + part) * 64 + (c & 15) + 16 * (lane >> 4)) * 8;
+            const size_t di = ((((size_t)T * 72 + kb) * 2 + part) * 64 + lane) * 8;
+            for (int j = 0; j < 8; ++j) dst[di + j] = src[si + j];
+          }
+  }
+  for (int T = 0; T < 16; ++T)
+    for (int kb = 0; kb < 3; ++kb)
+      for (int part = 0; part < 2; ++part)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int c = zrow_co(T, lane & 15);
+          const size_t si = ((((size_t)(c >> 4) * 3 + kb) * 2 + part) * 64 + (c & 15) + 16 * (lane >> 4)) * 8;
+          const size_t di = ((((size_t)T * 3 + kb) * 2 + part) * 64 + lane) * 8;
+          for (int j = 0; j < 8; ++j) sz[di + j] = sy[si + j];
+        }
   // k_net_y output bounds (NetWeights::yrange): per conv the max over output channels of the
   // L1 norm of the folded weights and the max |folded bias|; the stem's; max |embedding|.
   std::vector<float> yr(2 * CONV_LAYERS + 3);
@@ -1003,8 +1027,9 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.yrange = h->wyrange;
   const size_t nx = wy.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
   const size_t nsc = (sc8.size() + 3) / 4, n6 = w6.size() / 16;
-  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6
-  const size_t o_sy = nx, o_w8 = o_sy + nsy, o_sc = o_w8 + n8, o_w6 = o_sc + nsc, o_end = o_w6 + n6;
+  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6 | convz | stemz
+  const size_t o_sy = nx, o_w8 = o_sy + nsy, o_sc = o_w8 + n8, o_w6 = o_sc + nsc, o_wz = o_w6 + n6;
+  const size_t o_sz = o_wz + nx, o_end = o_sz + nsy;
   if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, o_end));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
   HIPCHK(hipMemcpy(h->wxbuf, wy.data(), nx * 16, hipMemcpyHostToDevice));
@@ -1012,6 +1037,8 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   HIPCHK(hipMemcpy(h->wxbuf + o_w8, w8.data(), n8 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_sc, sc8.data(), sc8.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_w6, w6.data(), n6 * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_wz, wz.data(), nx * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_sz, sz.data(), nsy * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx_inv = h->wxinv;
   h->w.stemx_inv = h->wxinv + CONV_LAYERS;
@@ -1020,6 +1047,8 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.conv8 = h->wxbuf + o_w8;
   h->w.conv8_sc = reinterpret_cast<const int32_t*>(h->wxbuf + o_sc);
   h->w.conv6 = h->wxbuf + o_w6;
+  h->w.convz = h->wxbuf + o_wz;
+  h->w.stemz = h->wxbuf + o_sz;
   h->weights_ok = true;
   return 0;
 }

@@ -179,14 +179,17 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
 
   // Epilogue: y = ReLU(acc * 2^(xs - e - xo) + bias * 2^-xo) in stored units; part 0 <- f16(y),
   // part 1 <- e4m3 copies of y - f16(y) and f16(y).  Conv A seeds conv B's accumulators with the
-  // block input Xh + Xl8 (conv B's units), read before its own store.
+  // block input Xh + Xl8 (conv B's units), read before its own store.  The weights' row order
+  // (NetWeights::convz) gives lane g of tile pair cp the 8 consecutive channels
+  // cb = 32 (CT/2 wc + cp) + 8 g .. cb + 7 (4 in each tile): per square one 16-B f16 store and two
+  // 8-B e4m3 stores.
   // boundb[bb]: rigorous bound on board bb's outputs (true units); the workgroup's xo follows
   // their max, as k_net_y's
   auto epilogue = [&](float inv, const float* bias, auto conv_a_t, float s_next, const float* boundb) {
     constexpr bool conv_a = decltype(conv_a_t)::value;
-    // the lane's coordinates, opaque here: otherwise the compiler hoists the epilogue's 48 LDS
+    // the lane's coordinates, opaque here: otherwise the compiler hoists the epilogue's LDS
     // addresses out of the layer loop and spills them, and every tile then waits on a scratch
-    // reload (about half of the epilogue's cycles)
+    // reload
     int el = lane;
     asm volatile("" : "+v"(el));
     const int n = el & 15, g = el >> 4, p1 = 16 + n;
@@ -216,72 +219,86 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
 #pragma unroll
     for (int j = 0; j < BPW; ++j) ymax[j] = 0.f;
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int co0 = 16 * CT * wc + 16 * ct + 4 * g;
-      const float4 bu = *reinterpret_cast<const float4*>(bias + co0);
-      const float4 bv = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
+    for (int cp = 0; cp < CT / 2; ++cp) {
+      const int cb = 32 * ((CT / 2) * wc + cp) + 8 * g;
+      float bv[8];
+      {
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + cb);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + cb + 4);
+        bv[0] = b0.x * st; bv[1] = b0.y * st; bv[2] = b0.z * st; bv[3] = b0.w * st;
+        bv[4] = b1.x * st; bv[5] = b1.y * st; bv[6] = b1.z * st; bv[7] = b1.w * st;
+      }
 #pragma unroll
       for (int t = 0; t < TW; ++t) {
         const int j = t >> 1, bb = wb0 + j, pt = t & 1;
-        f32x4v& a = acc[ct * TW + t];
+        f32x4v& a0 = acc[(2 * cp) * TW + t];
+        f32x4v& a1 = acc[(2 * cp + 1) * TW + t];
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
-          const int ah = zoff(0, bb, p, co0 >> 3) + 8 * (g & 1);
-          const int al8 = zoff(1, bb, p, co0 >> 4) + (co0 & 15);        // Xl8 bytes of co0..co0+3
-          const int ah8 = zoff(1, bb, p, 16 + (co0 >> 4)) + (co0 & 15); // Xh8
-          float y[4];
-          y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
-          y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
-          y[2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv.z), 0.f);
-          y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
-          ymax[j] = fmaxf(fmaxf(ymax[j], fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));
+          const int ah = zoff(0, bb, p, cb >> 3);                       // Xh: 16 B
+          const int al8 = zoff(1, bb, p, cb >> 4) + (cb & 15);          // Xl8: 8 B
+          const int ah8 = zoff(1, bb, p, 16 + (cb >> 4)) + (cb & 15);   // Xh8: 8 B
+          float y[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            y[i] = fmaxf(__builtin_fmaf(a0[i], in_scale, bv[i]), 0.f);
+            y[4 + i] = fmaxf(__builtin_fmaf(a1[i], in_scale, bv[4 + i]), 0.f);
+          }
+          ymax[j] = fmaxf(ymax[j], fmaxf(fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])),
+                                         fmaxf(fmaxf(y[4], y[5]), fmaxf(y[6], y[7]))));
           if constexpr (conv_a) {
-            const int xl = *reinterpret_cast<const int*>(smem + al8);
+            const uint2 xl = *reinterpret_cast<const uint2*>(smem + al8);
             if constexpr (NOMIX) {
-              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
-              a[0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[j]);
-              a[1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[j]);
-              a[2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[j]);
-              a[3] = __builtin_fmaf((float)xh[3], sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[j]);
+              const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ah);
+#define Z_SEED(A, X, I, O) A[I] = __builtin_fmaf((float)xh[(O) + (I)], sseed, __builtin_amdgcn_cvt_f32_fp8((int)X, I) * ls_in[j])
+              Z_SEED(a0, xl.x, 0, 0); Z_SEED(a0, xl.x, 1, 0); Z_SEED(a0, xl.x, 2, 0); Z_SEED(a0, xl.x, 3, 0);
+              Z_SEED(a1, xl.y, 0, 4); Z_SEED(a1, xl.y, 1, 4); Z_SEED(a1, xl.y, 2, 4); Z_SEED(a1, xl.y, 3, 4);
+#undef Z_SEED
             } else {
-              const uint2 xp = *reinterpret_cast<const uint2*>(smem + ah);
-              a[0] = zmix_lo(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 0) * ls_in[j]);
-              a[1] = zmix_hi(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 1) * ls_in[j]);
-              a[2] = zmix_lo(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 2) * ls_in[j]);
-              a[3] = zmix_hi(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8(xl, 3) * ls_in[j]);
+              const uint4 xp = *reinterpret_cast<const uint4*>(smem + ah);
+              a0[0] = zmix_lo(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.x, 0) * ls_in[j]);
+              a0[1] = zmix_hi(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.x, 1) * ls_in[j]);
+              a0[2] = zmix_lo(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.x, 2) * ls_in[j]);
+              a0[3] = zmix_hi(xp.y, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.x, 3) * ls_in[j]);
+              a1[0] = zmix_lo(xp.z, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.y, 0) * ls_in[j]);
+              a1[1] = zmix_hi(xp.z, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.y, 1) * ls_in[j]);
+              a1[2] = zmix_lo(xp.w, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.y, 2) * ls_in[j]);
+              a1[3] = zmix_hi(xp.w, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.y, 3) * ls_in[j]);
             }
           } else {
-            a = (f32x4v){0};
+            a0 = (f32x4v){0};
+            a1 = (f32x4v){0};
           }
-          f16x4 yh;
+          f16x8 yh;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) yh[q] = (_Float16)y[q];
-          float h[4], l[4];
+          for (int q = 0; q < 8; ++q) yh[q] = (_Float16)y[q];
+          float h[8], l[8];
           if constexpr (NOMIX) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < 8; ++q) {
               h[q] = (float)yh[q];
               l[q] = (y[q] - h[q]) * ls[j];   // exact difference, power-of-two scale
               h[q] *= hs[j];
             }
           } else {
             // l = y ls - h ls (= (y - h) ls, exact) and h hs straight from the packed halves
-            const uint2 yp = __builtin_bit_cast(uint2, yh);
+            const uint4 yp = __builtin_bit_cast(uint4, yh);
+            const uint32_t yw[4] = {yp.x, yp.y, yp.z, yp.w};
             const float nl = -ls[j];
-            l[0] = zmix_lo(yp.x, nl, y[0] * ls[j]);
-            l[1] = zmix_hi(yp.x, nl, y[1] * ls[j]);
-            l[2] = zmix_lo(yp.y, nl, y[2] * ls[j]);
-            l[3] = zmix_hi(yp.y, nl, y[3] * ls[j]);
-            h[0] = zmix_lo(yp.x, hs[j], 0.f);
-            h[1] = zmix_hi(yp.x, hs[j], 0.f);
-            h[2] = zmix_lo(yp.y, hs[j], 0.f);
-            h[3] = zmix_hi(yp.y, hs[j], 0.f);
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+              l[q] = zmix_lo(yw[q >> 1], nl, y[q] * ls[j]);
+              l[q + 1] = zmix_hi(yw[q >> 1], nl, y[q + 1] * ls[j]);
+              h[q] = zmix_lo(yw[q >> 1], hs[j], 0.f);
+              h[q + 1] = zmix_hi(yw[q >> 1], hs[j], 0.f);
+            }
           }
-          *reinterpret_cast<f16x4*>(smem + ah) = yh;
-          *reinterpret_cast<uint32_t*>(smem + al8) = pk_fp8x4(l[0], l[1], l[2], l[3]);
-          *reinterpret_cast<uint32_t*>(smem + ah8) = pk_fp8x4(h[0], h[1], h[2], h[3]);
+          *reinterpret_cast<f16x8*>(smem + ah) = yh;
+          *reinterpret_cast<uint2*>(smem + al8) = make_uint2(pk_fp8x4(l[0], l[1], l[2], l[3]), pk_fp8x4(l[4], l[5], l[6], l[7]));
+          *reinterpret_cast<uint2*>(smem + ah8) = make_uint2(pk_fp8x4(h[0], h[1], h[2], h[3]), pk_fp8x4(h[4], h[5], h[6], h[7]));
         } else {
-          a = (f32x4v){0};
+          a0 = (f32x4v){0};
+          a1 = (f32x4v){0};
         }
       }
     }
@@ -292,9 +309,9 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
 
   // VAR 8192 epilogue: the cross-term copies in e2m3 (fp6) blocks instead of e4m3 bytes.  The
   // wave's channel tiles pair up into 32-channel blocks blk = (CT/2) wc + bi (= K block 4c + g of
-  // the next conv's 128-channel chunk c), and per square its lane g holds channels 16 ct + 4 g + i
-  // (ct, i < 4) of the block: values 8 g + 4 ct + i of the block's 32-value fp6 vector
-  // (NetWeights::conv6 packs the weights in that order), bits 48 g .. 48 g + 47 = bytes 6 g .. 6 g + 5
+  // the next conv's 128-channel chunk c), and per square its lane g holds channels 8 g + 4 ct + i
+  // (ct < 2, i < 4) of the block (NetWeights::convz row order): values 8 g + 4 ct + i of the
+  // block's 32-value fp6 vector, bits 48 g .. 48 g + 47 = bytes 6 g .. 6 g + 5
   // of the 32-B block slot (term 0: Xl, chunks 2 blk, 2 blk + 1 of part 1; term 1: Xh, chunks
   // 16 + 2 blk, 17 + 2 blk), its e8m0 scale at byte 24.  The scale covers the block's largest
   // |value| (a rounded-up 16-bit key, max over the 4 lanes g), so that every value is <= 7.5 in
@@ -318,7 +335,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
       float4 bv[2];
   #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        const float4 bu = *reinterpret_cast<const float4*>(bias + 32 * blk + 16 * ct + 4 * g);
+        const float4 bu = *reinterpret_cast<const float4*>(bias + 32 * blk + 8 * g + 4 * ct);
         bv[ct] = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
       }
       // byte address of byte `b` of block blk's slot of term `term` on row p of board bb
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
               const uint32_t c = ct ? B24 : A24;
               uint32_t e = (c & 0x3fu) | ((c << 2) & 0x3f00u) | ((c << 4) & 0x3f0000u) | ((c << 6) & 0x3f000000u);
               e = (e & 0x1f1f1f1fu) | ((e & 0x20202020u) << 2);
-              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + zoff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1));
+              const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + zoff(0, bb, p, 4 * blk + g) + 8 * ct);
               xin[4 * ct + 0] = __builtin_fmaf((float)xh[0], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 0) * lsc);
               xin[4 * ct + 1] = __builtin_fmaf((float)xh[1], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 1) * lsc);
               xin[4 * ct + 2] = __builtin_fmaf((float)xh[2], sseed, __builtin_amdgcn_cvt_f32_fp8((int)e, 2) * lsc);
@@ -400,7 +417,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         if (valid) {
   #pragma unroll
           for (int ct = 0; ct < 2; ++ct)
-            *reinterpret_cast<f16x4*>(smem + zoff(0, bb, p, 4 * blk + 2 * ct + (g >> 1)) + 8 * (g & 1)) = yh[ct];
+            *reinterpret_cast<f16x4*>(smem + zoff(0, bb, p, 4 * blk + g) + 8 * ct) = yh[ct];
         }
   #pragma unroll
         for (int term = 0; term < 2; ++term) {
@@ -436,7 +453,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   stem_input<NT, true>(smem, simg, pos, b0, nb, W, tid);
   __syncthreads();
   {
-    const uint4* Ws = W.stemy + (size_t)(CT * wc) * 3 * 128 + lane;
+    const uint4* Ws = W.stemz + (size_t)(CT * wc) * 3 * 128 + lane;
     for (int kb = 0; kb < 3; ++kb) {
       f16x8 SA[2 * CT], SB[2 * TW];
 #pragma unroll
@@ -488,7 +505,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   f16x8 A16[RA][CT], B16[TW];
   i32x8 A8[RG][CT], B8[BPW];
   const int n_ = n, p1_ = p1, ph0_ = ph0, pw0_ = pw0, ph1_ = ph1, pw1_ = pw1, g_ = g;
-  const uint4* Wh = W.convy + (size_t)(CT * wc) * KBZ * 128 + lane;   // hi parts
+  const uint4* Wh = W.convz + (size_t)(CT * wc) * KBZ * 128 + lane;   // hi parts
   const uint4* W8 = W.conv8 + (size_t)(CT * wc) * GZ * 128 + lane;
   const uint4* W6 = W.conv6 + (size_t)(CT * wc) * GZ * 112;
   const int32_t* sc8 = W.conv8_sc;
