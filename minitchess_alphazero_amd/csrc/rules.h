@@ -3,7 +3,7 @@
 // Replaces the python-chess "minitchess" fork the reference consumes through
 // exp/environment.py:25-82 (Board(fen), legal_moves, push, result, fen).  The
 // rule content is the build's RULES.md (the fork is un-vendored);
-// bit-for-bit agreement with oracle/rules.py is tested (tests/test_rules_host.py
+// bit-for-bit agreement with oracle/rules.py is tested (tests/test_capi_cpu.py
 // on the CPU, tests/test_gpu_rules.py on the GPU).
 //
 // Geometry: 5 files x 6 ranks, square = 5*rank + file, bit `sq` of
