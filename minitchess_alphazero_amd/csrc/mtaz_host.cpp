@@ -1581,40 +1581,47 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (int g = 0; g < G; ++g) js[g] = (int32_t)K;
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs.data(), G * 8, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), G * 4, hipMemcpyHostToDevice, h->stream));
+    // chunks [0, 1), [1, 9), [9, 17), ...: the GPU starts after one draw per game, and each later
+    // chunk is drawn while the previous chunk's simulations run
     constexpr int NCH = 8;
-    auto draw_chunk = [&](int j0) {   // draws [j0, j0 + NCH) of every active game
+    auto chunk_end = [&](int j0) { return std::min(j0 == 0 ? 1 : j0 + NCH, h->sims); };
+    auto draw_chunk = [&](int j0) {   // draws [j0, chunk_end(j0)) of every active game
+      const int je = chunk_end(j0);
       parallel_for(G, [&](int g) {
         if (!active[g]) return;
-        const int k = root_k[g], jn = std::min(j0 + NCH, h->sims - root_new[g]);
+        const int k = root_k[g], jn = std::min(je, h->sims - root_new[g]);
         for (int j = j0; j < jn; ++j) legacy_dirichlet(h->rng[g], h->alpha, k, h->noise_host + (size_t)j * K + offs[g]);
       });
-      const int jn = std::min(j0 + NCH, h->sims);
-      if (jn > j0 && K > 0)
-        HIPCHK(hipMemcpyAsync(h->d.gm.noise + (size_t)j0 * K, h->noise_host + (size_t)j0 * K, (size_t)(jn - j0) * K * 8,
+      if (je > j0 && K > 0)
+        HIPCHK(hipMemcpyAsync(h->d.gm.noise + (size_t)j0 * K, h->noise_host + (size_t)j0 * K, (size_t)(je - j0) * K * 8,
                               hipMemcpyHostToDevice, h->stream));
       return 0;
     };
     ECHK(draw_chunk(0));
     rng_ms += now_ms() - tr;
-    for (int s0 = 0; s0 < h->sims; s0 += NCH) {
-      // simulation s uses draw s - root_new <= s: chunk s0 / NCH is on the stream before them
-      for (int s = s0; s < std::min(s0 + NCH, h->sims); ++s) ECHK(sim_gpu(h, s));
-      if (s0 + NCH < h->sims) {
+    for (int s0 = 0; s0 < h->sims; s0 = chunk_end(s0)) {
+      // simulation s uses draw s - root_new <= s: the chunk holding draw s is on the stream first
+      for (int s = s0; s < chunk_end(s0); ++s) ECHK(sim_gpu(h, s));
+      if (chunk_end(s0) < h->sims) {
         tr = now_ms();
-        ECHK(draw_chunk(s0 + NCH));
+        ECHK(draw_chunk(chunk_end(s0)));
         rng_ms += now_ms() - tr;
       }
     }
+    // root visit counts, rows of the longest active legal list (not KMAX: 8x fewer bytes to the host)
+    int kmx = 1;
+    for (int g = 0; g < G; ++g)
+      if (active[g]) kmx = std::max(kmx, root_k[g]);
     ts = now_ms();
-    ECHK(mtaz_move_end(h, codes.data(), visits.data(), nullptr, KMAX));
+    ECHK(mtaz_move_end(h, codes.data(), visits.data(), nullptr, kmx));
     sync_ms += now_ms() - ts;
     // action selection (exp/agent.py:110-119) + records (exp/callbacks.py:40-47)
     tr = now_ms();
     parallel_for(G, [&](int g) {
       if (!active[g]) return;
       const int k = root_k[g];
-      const uint16_t* c = codes.data() + (size_t)g * KMAX;
-      const uint32_t* v = visits.data() + (size_t)g * KMAX;
+      const uint16_t* c = codes.data() + (size_t)g * kmx;
+      const uint32_t* v = visits.data() + (size_t)g * kmx;
       double pi[KMAX];
       double sum = 0;
       for (int i = 0; i < k; ++i) sum += (double)v[i];

@@ -4,6 +4,8 @@
 relatively); the explainer runs with that deviation as its tolerance.  Where the perturbed game
 leaves the unperturbed one, it must find the first differing PUCT selection and report a near-tie
 inside the tolerance bound, and a 100x smaller tolerance must not explain it."""
+import zlib
+
 import numpy as np
 
 from helpers import compare_records, explain_divergence
@@ -15,7 +17,7 @@ class _Perturbed:
 
     def evaluate(self, fen, legal):
         P, v = self.base.evaluate(fen, legal)
-        h = abs(hash(fen)) % 1000 / 1000.0 - 0.5
+        h = zlib.crc32(fen.encode()) % 1000 / 1000.0 - 0.5   # (not hash(): salted per process)
         P = np.asarray(P, np.float64) * (1 + self.eps * h)
         P = (P / P.sum()).astype(np.float32)
         v = float(np.float32(v + self.eps * h))
@@ -28,7 +30,7 @@ def test_explainer_finds_an_explained_near_tie():
     from oracle.mcts import SyntheticEvaluator
     base = SyntheticEvaluator(salt=7)
     found = False
-    for seed in range(20):
+    for seed in (30, 36, 52, 58):   # seeds whose perturbed game diverges (deterministic perturbation)
         table = {}
         gpu = selfplay.play_games(_Perturbed(base, 2e-4, table), 1, 32, seed_base=seed)[0]
         ref = selfplay.play_games(base, 1, 32, seed_base=seed)[0]
