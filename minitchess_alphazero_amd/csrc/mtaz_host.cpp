@@ -15,6 +15,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -443,6 +447,73 @@ enum Stat {
   ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_COUNT
 };
 
+// Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
+// thread (the main thread, or each stream group's thread), created on first use and joined when
+// that thread exits, so a move does not pay for starting threads.  Workers 1..nt-1 take equal
+// contiguous ranges; the calling thread runs range 0.
+class HostPool {
+ public:
+  explicit HostPool(int nt) : nt_(nt) {
+    for (int t = 1; t < nt_; ++t) th_.emplace_back([this, t] { worker(t); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& x : th_) x.join();
+  }
+  int size() const { return nt_; }
+  void run(int n, const std::function<void(int)>& f) {
+    const int chunk = (n + nt_ - 1) / nt_;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &f;
+      n_ = n;
+      chunk_ = chunk;
+      pending_ = nt_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (int i = 0; i < std::min(n, chunk); ++i) f(i);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void worker(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      int a, b;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+        a = t * chunk_;
+        b = std::min(n_, a + chunk_);
+      }
+      for (int i = a; i < b; ++i) (*f)(i);
+      {
+        std::lock_guard<std::mutex> lk(m_);
+        if (--pending_ == 0) done_.notify_one();
+      }
+    }
+  }
+  int nt_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int n_ = 0, chunk_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 template <class F>
 void parallel_for(int n, F f) {
   int nt = (int)std::thread::hardware_concurrency();
@@ -451,14 +522,10 @@ void parallel_for(int n, F f) {
     for (int i = 0; i < n; ++i) f(i);
     return;
   }
-  std::vector<std::thread> th;
-  const int chunk = (n + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t) {
-    const int a = t * chunk, b = std::min(n, a + chunk);
-    if (a >= b) break;
-    th.emplace_back([=, &f]() { for (int i = a; i < b; ++i) f(i); });
-  }
-  for (auto& x : th) x.join();
+  thread_local std::unique_ptr<HostPool> pool;
+  if (!pool) pool.reset(new HostPool(nt));
+  const std::function<void(int)> fn = [&f](int i) { f(i); };
+  pool->run(n, fn);
 }
 
 double now_ms() {
