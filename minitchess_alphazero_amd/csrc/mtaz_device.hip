@@ -74,6 +74,7 @@ __device__ int wave_legal(const BB& b, uint32_t flags, const RuleTables& RT, Leg
   const int cnt = popc(ps);
   const int incl = wave_incl_scan(cnt);
   const int nps = __shfl(incl, 63, 64);     // <= 15 * 15: own pieces x other squares
+  if (nps > KMAX) return -1;                // (unreachable from legal play; keeps L.pm in bounds)
   int off = incl - cnt;
   for (uint32_t m = ps; m; m &= m - 1) L.pm[off++] = (uint16_t)(lane | (lsb(m) << 8));
   __syncthreads();
