@@ -109,6 +109,18 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // 2097152: the e4m3 epilogue's unfused form (product: v_fma_mix for the lo part, the Xh copy and
   // the residual seed; bit-identical, test_gpu_net.py test_z_mix_epilogue_bit_identical)
   constexpr bool NOMIX = (VAR & 2097152) != 0;
+  // K-loop form.  Product: tap-major (one tap = 8 steps per iteration; a fragment's LDS offset is a
+  // per-tap base plus a step constant, selected against the zero cell by the tap's on-board mask,
+  // 2-3 VALU per address) with the weight fragments by buffer loads (descriptor + per-wave lane
+  // offset, the layer / step offset in an SGPR).  8388608 = the round-2 loop (the source square's
+  // offset recomputed per step and fragment), 16777216 = weights by 64-bit global addresses; all
+  // four forms bit-identical (test_z_loop_forms_bit_identical).  31 -> 11 VALU and 17 -> 7 SALU
+  // per step: -8.5% workgroup cycles, -5.7% launch time (profiles/r02_tap/).
+  constexpr int RA0 = (NW == 8 ? 1 : 2) + 1;   // the A16 ring (PD + 1, below)
+  // (The e2m3 build spills some registers in either loop, 18 in the round-2 one and 23 in the
+  // tap-major one, which is still 5% faster; with buffer-loaded weights it spills 30.)
+  constexpr bool TAPA = (VAR & 8388608) == 0 && !DIAG_NOLDS && RA0 == 2;
+  constexpr bool WBUF = (VAR & 16777216) == 0 && !F6;
   __shared__ __attribute__((aligned(16))) char smem[ZIMGB + AUXB];
   const int nb = count ? *count : max_b;
   const int b0 = blockIdx.x * XB;
@@ -510,13 +522,24 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   const uint4* W6 = W.conv6 + (size_t)(CT * wc) * GZ * 112;
   const int32_t* sc8 = W.conv8_sc;
   const int bofs = wb0 * ZBOARD;   // the wave's first board in each image part
+  // WBUF: buffer descriptors of the f16 and e4m3 weight sets, the wave's lane offsets and the
+  // layer's byte offsets (both sets < 2 GB)
+  const __amdgpu_buffer_rsrc_t rs_h = __builtin_amdgcn_make_buffer_rsrc((void*)W.convz, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_8 = __builtin_amdgcn_make_buffer_rsrc((void*)W.conv8, (short)0, 0x7ffffff0, 0x00020000);
+  const int vo_h = (CT * wc * KBZ * 128 + lane) * 16, vo_8 = (CT * wc * GZ * 128 + lane) * 16;
+  int lo_h = 0, lo_8 = 0;
 
   // Wh fragments of step (k-block) KB, the wave's channel tiles
 #define Z_LOAD_A16(S, KB)                                                             \
   {                                                                                   \
     const int kk_ = DIAG_L1 ? 0 : (KB) < KBZ ? (KB) : KBZ - 1;                        \
-    _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_)                                 \
-      S[c_] = __builtin_bit_cast(f16x8, Wh[((size_t)c_ * KBZ + kk_) * 128]);          \
+    _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_) {                               \
+      if constexpr (WBUF)                                                             \
+        S[c_] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(       \
+                    rs_h, vo_h, lo_h + (c_ * KBZ + kk_) * 2048, 0));                  \
+      else                                                                            \
+        S[c_] = __builtin_bit_cast(f16x8, Wh[((size_t)c_ * KBZ + kk_) * 128]);        \
+    }                                                                                 \
   }
   // e4m3 weight fragments of group GR (tap, chunk, term), channel tiles [C0, C0 + CT/2); with
   // F6 the e2m3 vector in dwords 0..5 and the lane's e8m0 scale in dword 6
@@ -531,6 +554,12 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         const uint32_t sc_ = reinterpret_cast<const uint32_t*>(p_ + 96)[lane];        \
         S[c_] = (i32x8){(int)d0_.x, (int)d0_.y, (int)d0_.z, (int)d0_.w,               \
                         (int)d1_.x, (int)d1_.y, (int)sc_, 0};                         \
+      } else if constexpr (WBUF) {                                                    \
+        const int so_ = lo_8 + (c_ * GZ + gg_) * 2048;                                \
+        const auto a_ = __builtin_amdgcn_raw_buffer_load_b128(rs_8, vo_8, so_, 0);    \
+        const auto b_ = __builtin_amdgcn_raw_buffer_load_b128(rs_8, vo_8 + 1024, so_, 0); \
+        S[c_] = (i32x8){(int)a_[0], (int)a_[1], (int)a_[2], (int)a_[3],               \
+                        (int)b_[0], (int)b_[1], (int)b_[2], (int)b_[3]};              \
       } else {                                                                        \
         const uint4* p_ = W8 + ((size_t)c_ * GZ + gg_) * 128;                         \
         S[c_] = cat8(p_[0], p_[64]);                                                  \
@@ -586,6 +615,93 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
       Z_LOAD_A8(A8[p], p, 0)
       Z_LOAD_A8(A8[p], p, CT / 2)
     }
+    if constexpr (TAPA) {
+      static_assert(RA == 2 && RG == 2 && !DIAG_NOLDS, "tap-major loop: 8 steps per iteration");
+      // per tap and square tile: the source square's chunk-0 row offset, its zero cell and the
+      // on-board mask (as zsrc); a fragment's offset = mask ? row + chunk offset : zero cell
+      const int g256 = g << 8, g512 = g << 9;
+      auto zsel = [](int m, int on, int off) { return (on & m) | (off & ~m); };
+      auto tap_addr = [&](int t, int* row, int* off, int* m) {
+        const int dh = t / 3 - 1, dw = t - 3 * (t / 3) - 1;
+        const int pp[2] = {n, p1}, hh[2] = {ph0, ph1}, ww[2] = {pw0, pw1};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = hh[i] + dh, c = ww[i] + dw, s = pp[i] + 5 * dh + dw;
+          const bool valid = (pp[i] < 30) & ((unsigned)r < 6u) & ((unsigned)c < 5u);
+          row[i] = 8192 * (s >> 4) + 16 * (s & 15);
+          off[i] = ZROWS_B + 16 * (s & 15);
+          m[i] = valid ? -1 : 0;
+        }
+      };
+      int crow[2], coff[2], cm[2];
+      tap_addr(0, crow, coff, cm);
+      // Xh fragments of chunk-step CS (0..7) of a tap: channels 4 CS + g of 32-channel block
+#define Z_LOAD_B16T(S16, ROW, OFF, M, CS)                                                  \
+  {                                                                                       \
+    const int o0_ = zsel(M[0], ROW[0] + g256 + 1024 * (CS), OFF[0]);                      \
+    const int o1_ = zsel(M[1], ROW[1] + g256 + 1024 * (CS), OFF[1]);                      \
+    _Pragma("unroll") for (int j_ = 0; j_ < BPW; ++j_) {                                  \
+      const char* base_ = smem + bofs + j_ * ZBOARD;                                      \
+      S16[2 * j_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                         \
+      S16[2 * j_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);                     \
+    }                                                                                     \
+  }
+      Z_LOAD_B16T(B16, crow, coff, cm, 0);
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t) {
+        int nrow[2], noff[2], nm[2];
+        tap_addr(t < 8 ? t + 1 : 8, nrow, noff, nm);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int s = 8 * t + u;
+          __builtin_amdgcn_sched_barrier(0);
+          {
+            // e4m3 fragments of step s (group s/2 = term (u>>1)&1, chunk (u>>2)&1, tile u&1):
+            // channels [128 cc + 32 g, +32) of part 1's Xl8 (term 0) or Xh8 (term 1) block
+            const int tl = u & 1;
+            const int z0 = zsel(cm[tl], crow[tl] + g512 + 4096 * ((u >> 1) & 1) + 2048 * ((u >> 2) & 1), coff[tl]);
+            const char* p0 = smem + ZPART + bofs + z0;
+#pragma unroll
+            for (int j = 0; j < BPW; ++j)
+              B8[j] = cat8(*reinterpret_cast<const uint4*>(p0 + j * ZBOARD),
+                           *reinterpret_cast<const uint4*>(p0 + j * ZBOARD + 256));
+          }
+          Z_LOAD_A16(A16[(u + PD) % RA], s + PD);
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int tt = 0; tt < TW; ++tt)
+              acc[ct * TW + tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A16[u % RA][ct], B16[tt], acc[ct * TW + tt], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (u < 7)
+            Z_LOAD_B16T(B16, crow, coff, cm, u + 1)
+          else
+            Z_LOAD_B16T(B16, nrow, noff, nm, 0)
+          Z_LOAD_A8(A8[((u >> 1) + GD) % RG], (s >> 1) + GD, (CT / 2) * (u & 1));
+          const int pt = u & 1;
+          const bool term = (u >> 1) & 1;
+          const int sa = term ? sa_l : sa_h;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int j = 0; j < BPW; ++j) {
+              if constexpr (DIAG_NOB)
+                ;
+              else if constexpr (F6)
+                acc[ct * TW + 2 * j + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    A8[(u >> 1) % RG][ct], B8[j], acc[ct * TW + 2 * j + pt], 2, 2, 0, A8[(u >> 1) % RG][ct][6], 0,
+                    B8[j][6]);
+              else
+                acc[ct * TW + 2 * j + pt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    A8[(u >> 1) % RG][ct], B8[j], acc[ct * TW + 2 * j + pt], 0, 0, 0, sa, 0,
+                    term ? sb_h[j] : sb_l[j]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) crow[i] = nrow[i], coff[i] = noff[i], cm[i] = nm[i];
+      }
+#undef Z_LOAD_B16T
+    } else {
     Z_LOAD_B16(B16, 0);
     if constexpr (DIAG_NOLDS) Z_LOAD_B8(B8, 0);
     {
@@ -630,9 +746,12 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         }
       }
     }
+    }
     if constexpr (!DIAG_L2 && !DIAG_L1) {
       Wh += CONVX_U4_PER_LAYER;
       W8 += CONV8_U4_PER_LAYER;
+      lo_h += (int)(CONVX_U4_PER_LAYER * 16);
+      lo_8 += (int)(CONV8_U4_PER_LAYER * 16);
       W6 += CONV6_U4_PER_LAYER;
     }
     __syncthreads();
@@ -689,10 +808,14 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      unsigned long long* stamps) {
 #define Z_LAUNCH(V, T)                                                                                       \
   hipLaunchKernelGGL((k_net_z<S, V>), grid, dim3(T), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps)
-  // product builds (mtaz_set_net_variant accepts these): 0, the unfused epilogue, e2m3 cross terms
+  // product builds (mtaz_set_net_variant accepts these): 0, the unfused epilogue, e2m3 cross terms,
+  // the round-2 K loop (per-step addresses, global-address weights)
   if (var == 2097152) Z_LAUNCH(2097152, 512);
   else if (var == 8192) Z_LAUNCH(8192, 512);
+  else if (var == 8388608 + 16777216) Z_LAUNCH(8388608 + 16777216, 512);
 #ifdef MTAZ_NET_DIAG
+  else if (var == 8388608) Z_LAUNCH(8388608, 512);
+  else if (var == 16777216) Z_LAUNCH(16777216, 512);
   else if (var == 4194304) Z_LAUNCH(4194304, 512);
   else if (var == 4194304 + 8192) Z_LAUNCH(4194304 + 8192, 512);
   // A/B and timing-only builds: the diagnostic library only (tools/bench_net.py --diag)

@@ -29,13 +29,15 @@ __device__ __forceinline__ int ioff(int part, int bb, int row, int chunk) {
 // within 16-row halves: (row r, chunk q) at 256 (q + 32 (r >> 4)) + 16 (r & 15).  The bank group
 // of a 16-B chunk then depends on its row alone, and a K-loop fragment read (each 16-lane read
 // group = the 16 consecutive output squares of a tile, any chunk per lane) touches 16 distinct
-// rows: conflict-free.  Off-board taps read a per-lane cell of the board's zero line (256 B after
-// the rows), on the bank the on-board source would have had (tools/lds_conflicts.py: 4.0 LDS
-// cycles per ds_read_b128 against 6.9 / 7.6 for the row-major swizzled image).
+// rows: conflict-free.  Off-board taps read a per-lane cell of the board's zero line (after the
+// rows), on the bank the on-board source would have had (tools/lds_conflicts.py: 4.0 LDS
+// cycles per ds_read_b128 against 6.9 / 7.6 for the row-major swizzled image).  The zero line is
+// two chunks wide (512 B), so that an e4m3 fragment's second 16-B read is always its first read's
+// address + 256, on-board (the next chunk) or off (the second zero cell).
 constexpr int ZROWS_B = 16384;                 // bytes of rows per board and part
-constexpr int ZBOARD = ZROWS_B + 256;          // + the zero line
-constexpr int ZPART = XB * ZBOARD;             // 66,560 B per part
-constexpr int ZIMGB = 2 * ZPART;               // 133,120 B
+constexpr int ZBOARD = ZROWS_B + 512;          // + the zero line
+constexpr int ZPART = XB * ZBOARD;             // 67,584 B per part
+constexpr int ZIMGB = 2 * ZPART;               // 135,168 B
 __device__ __forceinline__ int zrow(int row, int chunk) { return 256 * (chunk + 32 * (row >> 4)) + 16 * (row & 15); }
 __device__ __forceinline__ int zoff(int part, int bb, int row, int chunk) {
   return part * ZPART + bb * ZBOARD + zrow(row, chunk);
@@ -80,8 +82,8 @@ template <int NT = 256, bool ZL = false>
 __device__ __forceinline__ void stem_input(char* smem, char* simg, const Pos* pos, int b0, int nb,
                                            const NetWeights& W, int tid) {
   if constexpr (ZL) {   // the zero lines
-    for (int i = tid; i < 2 * XB * 16; i += NT) {
-      const int part = i / (XB * 16), bb = (i / 16) % XB, c = i & 15;
+    for (int i = tid; i < 2 * XB * 32; i += NT) {
+      const int part = i / (XB * 32), bb = (i / 32) % XB, c = i & 31;
       *reinterpret_cast<uint4*>(smem + part * ZPART + bb * ZBOARD + ZROWS_B + 16 * c) = make_uint4(0, 0, 0, 0);
     }
   } else {

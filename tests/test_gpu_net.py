@@ -115,7 +115,8 @@ def test_product_library_rejects_untested_variants():
     from minitchess_alphazero_amd import _lib
     from minitchess_alphazero_amd.engine import Engine
     eng = Engine(n_games=4, sims=2)
-    for prec, good, bad in (('f16f8', [0, 8192, 2097152], [16384, 32768, 65536, 131072, 2048, 4194304]),
+    for prec, good, bad in (('f16f8', [0, 8192, 2097152, 25165824],
+                             [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
                             ('f16x3', [0, 1024], [512, 4, 8, 2048, 8192])):
         eng.set_precision(prec)
         for v in good:
@@ -148,6 +149,66 @@ def test_z_mix_epilogue_bit_identical():
         l1, v1 = eng.evaluate(pos)
         assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
         assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
+def test_z_loop_forms_bit_identical():
+    """k_net_z's tap-major K loop with buffer-loaded weights (the product) computes exactly the
+    round-2 loop (per-step fragment addresses, 64-bit global weight addresses; variant 25165824):
+    logits and values bitwise equal on an ordinary, a wide-range and a tiny-activation net."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from minitchess_alphazero_amd.network import Network
+    from tests_positions import random_fens
+    import torch
+    torch.manual_seed(0)
+    pos = np.stack([pos_from_fen(f) for f in random_fens(259, seed=13)])
+    for net in (Network(), _wide_range_net(), _tiny_activation_net()):
+        eng = Engine(n_games=64, sims=4)
+        eng.set_precision('f16f8')
+        eng.set_weights(net)
+        eng.set_net_variant(0)
+        l0, v0 = eng.evaluate(pos)
+        eng.set_net_variant(25165824)
+        l1, v1 = eng.evaluate(pos)
+        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
+def _tiny_activation_net(scale=2.0 ** -20):
+    """Random-init net with every BatchNorm gamma and beta x `scale` (stem and both convs of every
+    block): folded weights and biases shrink with it, so the trunk's activations sit around
+    1e-6, in f16's subnormal range, where the v_fma_mix forms read subnormal halves."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    with torch.no_grad():
+        bns = [net.resbody[0].layers[1]]
+        for blk in list(net.resbody)[1:]:
+            bns += [blk.convblock1.layers[1], blk.convblock2.layers[1]]
+        for bn in bns:
+            bn.weight.mul_(scale)
+            bn.bias.mul_(scale)
+    return net.eval()
+
+
+@pytest.mark.parametrize('precision,var0,var1', [('f16f8', 0, 2097152), ('f16x3', 0, 1024)])
+def test_mix_epilogue_bit_identical_tiny_activations(precision, var0, var1):
+    """The v_fma_mix epilogues equal their unfused forms bitwise also when the activations are
+    f16-subnormal (the mix path's exactness precondition)."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from tests_positions import random_fens
+    eng = Engine(n_games=64, sims=4)
+    eng.set_precision(precision)
+    eng.set_weights(_tiny_activation_net())
+    pos = np.stack([pos_from_fen(f) for f in random_fens(97, seed=6)])
+    eng.set_net_variant(var0)
+    l0, v0 = eng.evaluate(pos)
+    eng.set_net_variant(var1)
+    l1, v1 = eng.evaluate(pos)
+    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
 
 
 def _wide_range_net(gain=6.0):
