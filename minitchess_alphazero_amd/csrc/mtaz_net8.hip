@@ -57,6 +57,22 @@ __device__ __forceinline__ float zmix_hi(uint32_t pk, float b, float c) {
   return r;
 }
 
+typedef short zv2i16 __attribute__((ext_vector_type(2)));
+typedef _Float16 zv2f16 __attribute__((ext_vector_type(2)));
+// gfx950's scaled conversions: e4m3 of x / s (encode) and x * s (decode) for a power-of-two s,
+// bitwise the unscaled conversion of the exactly scaled value (tools/probes/cvt_scale_probe.hip,
+// profiles/r02_tap/cvt_scale_probe.json: 65,536 random pairs per scale 2^-24..2^24, all equal)
+__device__ __forceinline__ uint32_t sc_fp8x4(float a, float b, float c, float d, float s) {
+  zv2i16 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32((zv2i16){0, 0}, a, b, s, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, c, d, s, true);
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t sc_fp8x4_f16(uint32_t h01, uint32_t h23, float s) {
+  zv2i16 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16((zv2i16){0, 0}, __builtin_bit_cast(zv2f16, h01), s, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(r, __builtin_bit_cast(zv2f16, h23), s, true);
+  return __builtin_bit_cast(uint32_t, r);
+}
+
 // 4 e4m3 bytes of {a, b, c, d} (round to nearest even, OCP e4m3fn)
 __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d) {
   int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
@@ -109,6 +125,11 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // 2097152: the e4m3 epilogue's unfused form (product: v_fma_mix for the lo part, the Xh copy and
   // the residual seed; bit-identical, test_gpu_net.py test_z_mix_epilogue_bit_identical)
   constexpr bool NOMIX = (VAR & 2097152) != 0;
+  // Product epilogue: its power-of-two scalings folded into gfx950's scaled conversions (the Xl8 /
+  // Xh8 copies and the residual seed's Xl8 decode; -35% epilogue VALU).  33554432 = the round-2
+  // form (v_fma_mix scalings, unscaled conversions); bit-identical (test_z_mix_epilogue_bit_identical
+  // against the unfused form)
+  constexpr bool SCVT = (VAR & 33554432) == 0 && !NOMIX && !F6;   // (e2m3: more spills with it)
   // K-loop form.  Product: tap-major (one tap = 8 steps per iteration; a fragment's LDS offset is a
   // per-tap base plus a step constant, selected against the zero cell by the tap's on-board mask,
   // 2-3 VALU per address) with the weight fragments by buffer loads (descriptor + per-wave lane
@@ -116,10 +137,12 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // offset recomputed per step and fragment), 16777216 = weights by 64-bit global addresses; all
   // four forms bit-identical (test_z_loop_forms_bit_identical).  31 -> 11 VALU and 17 -> 7 SALU
   // per step: -8.5% workgroup cycles, -5.7% launch time (profiles/r02_tap/).
-  constexpr int RA0 = (NW == 8 ? 1 : 2) + 1;   // the A16 ring (PD + 1, below)
+  // 67108864: Wh fragments 3 steps ahead instead of 1 (tap-major loop only)
+  constexpr bool PD3 = (VAR & 67108864) != 0;
+  constexpr int RA0 = (NW == 8 ? (PD3 ? 3 : 1) : 2) + 1;   // the A16 ring (PD + 1, below)
   // (The e2m3 build spills some registers in either loop, 18 in the round-2 one and 23 in the
   // tap-major one, which is still 5% faster; with buffer-loaded weights it spills 30.)
-  constexpr bool TAPA = (VAR & 8388608) == 0 && !DIAG_NOLDS && RA0 == 2;
+  constexpr bool TAPA = (VAR & 8388608) == 0 && !DIAG_NOLDS && 8 % RA0 == 0;
   constexpr bool WBUF = (VAR & 16777216) == 0 && !F6;
   __shared__ __attribute__((aligned(16))) char smem[ZIMGB + AUXB];
   const int nb = count ? *count : max_b;
@@ -212,7 +235,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
     // board bb's stored values are <= boundb[bb] * 2^-xo =: bs; sh_new = 7 - ilogb(bs) keeps
     // e4m3(Xh * 2^sh) < 256 (clamped so that 2^(sh + 11) stays a normal float)
     int sh_new[XB];
-    float hs[BPW], ls[BPW], ls_in[BPW];
+    float hs[BPW], ls[BPW], ls_in[BPW], ihs[BPW], ils[BPW];
 #pragma unroll
     for (int bb = 0; bb < XB; ++bb) {
       const float bs = __builtin_ldexpf(boundb[bb], -xo);
@@ -225,6 +248,8 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
       const int snew = pick4(sh_new, wb0 + j), sold = pick4(sh, wb0 + j);
       hs[j] = __builtin_ldexpf(1.f, snew);
       ls[j] = __builtin_ldexpf(1.f, snew + 11);
+      ihs[j] = __builtin_ldexpf(1.f, -snew);
+      ils[j] = __builtin_ldexpf(1.f, -(snew + 11));
       ls_in[j] = __builtin_ldexpf(sseed, -(sold + 11));   // Xl8 units of the image being read
     }
     float ymax[BPW];
@@ -266,6 +291,20 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
               Z_SEED(a0, xl.x, 0, 0); Z_SEED(a0, xl.x, 1, 0); Z_SEED(a0, xl.x, 2, 0); Z_SEED(a0, xl.x, 3, 0);
               Z_SEED(a1, xl.y, 0, 4); Z_SEED(a1, xl.y, 1, 4); Z_SEED(a1, xl.y, 2, 4); Z_SEED(a1, xl.y, 3, 4);
 #undef Z_SEED
+            } else if constexpr (SCVT) {
+              const uint4 xp = *reinterpret_cast<const uint4*>(smem + ah);
+              const auto d0 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(xl.x, ls_in[j], false);
+              const auto d1 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(xl.x, ls_in[j], true);
+              const auto d2 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(xl.y, ls_in[j], false);
+              const auto d3 = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(xl.y, ls_in[j], true);
+              a0[0] = zmix_lo(xp.x, sseed, d0[0]);
+              a0[1] = zmix_hi(xp.x, sseed, d0[1]);
+              a0[2] = zmix_lo(xp.y, sseed, d1[0]);
+              a0[3] = zmix_hi(xp.y, sseed, d1[1]);
+              a1[0] = zmix_lo(xp.z, sseed, d2[0]);
+              a1[1] = zmix_hi(xp.z, sseed, d2[1]);
+              a1[2] = zmix_lo(xp.w, sseed, d3[0]);
+              a1[3] = zmix_hi(xp.w, sseed, d3[1]);
             } else {
               const uint4 xp = *reinterpret_cast<const uint4*>(smem + ah);
               a0[0] = zmix_lo(xp.x, sseed, __builtin_amdgcn_cvt_f32_fp8((int)xl.x, 0) * ls_in[j]);
@@ -284,6 +323,24 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
           f16x8 yh;
 #pragma unroll
           for (int q = 0; q < 8; ++q) yh[q] = (_Float16)y[q];
+          if constexpr (SCVT) {
+            // d = y - h exactly (Sterbenz), Xl8 = e4m3(d * ls), Xh8 = e4m3(h * hs) by the scaled
+            // conversions (x / s: s = 1 / ls, 1 / hs, powers of two)
+            const uint4 yp = __builtin_bit_cast(uint4, yh);
+            const uint32_t yw[4] = {yp.x, yp.y, yp.z, yp.w};
+            float d[8];
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+              d[q] = zmix_lo(yw[q >> 1], -1.f, y[q]);
+              d[q + 1] = zmix_hi(yw[q >> 1], -1.f, y[q + 1]);
+            }
+            *reinterpret_cast<f16x8*>(smem + ah) = yh;
+            *reinterpret_cast<uint2*>(smem + al8) = make_uint2(sc_fp8x4(d[0], d[1], d[2], d[3], ils[j]),
+                                                               sc_fp8x4(d[4], d[5], d[6], d[7], ils[j]));
+            *reinterpret_cast<uint2*>(smem + ah8) = make_uint2(sc_fp8x4_f16(yw[0], yw[1], ihs[j]),
+                                                               sc_fp8x4_f16(yw[2], yw[3], ihs[j]));
+            continue;
+          }
           float h[8], l[8];
           if constexpr (NOMIX) {
 #pragma unroll
@@ -511,7 +568,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   if constexpr (PRIO) {
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
-  constexpr int PD = NW == 8 ? 1 : 2, RA = PD + 1, GD = 1, RG = GD + 1;
+  constexpr int PD = RA0 - 1, RA = PD + 1, GD = 1, RG = GD + 1;
   constexpr int U = (RA == 2 && RG == 2) ? 4 : 12;
   static_assert(KBZ % U == 0 && U % RA == 0 && (U / 2) % RG == 0 && RG > GD, "rings");
   f16x8 A16[RA][CT], B16[TW];
@@ -616,7 +673,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
       Z_LOAD_A8(A8[p], p, CT / 2)
     }
     if constexpr (TAPA) {
-      static_assert(RA == 2 && RG == 2 && !DIAG_NOLDS, "tap-major loop: 8 steps per iteration");
+      static_assert(8 % RA == 0 && RG == 2 && !DIAG_NOLDS, "tap-major loop: 8 steps per iteration");
       // per tap and square tile: the source square's chunk-0 row offset, its zero cell and the
       // on-board mask (as zsrc); a fragment's offset = mask ? row + chunk offset : zero cell
       const int g256 = g << 8, g512 = g << 9;
@@ -812,6 +869,8 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
   // the round-2 K loop (per-step addresses, global-address weights)
   if (var == 2097152) Z_LAUNCH(2097152, 512);
   else if (var == 8192) Z_LAUNCH(8192, 512);
+  else if (var == 33554432) Z_LAUNCH(33554432, 512);
+  else if (var == 67108864) Z_LAUNCH(67108864, 512);
   else if (var == 8388608 + 16777216) Z_LAUNCH(8388608 + 16777216, 512);
 #ifdef MTAZ_NET_DIAG
   else if (var == 8388608) Z_LAUNCH(8388608, 512);

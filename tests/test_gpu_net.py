@@ -115,7 +115,7 @@ def test_product_library_rejects_untested_variants():
     from minitchess_alphazero_amd import _lib
     from minitchess_alphazero_amd.engine import Engine
     eng = Engine(n_games=4, sims=2)
-    for prec, good, bad in (('f16f8', [0, 8192, 2097152, 25165824],
+    for prec, good, bad in (('f16f8', [0, 8192, 2097152, 25165824, 33554432, 67108864],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
                             ('f16x3', [0, 1024], [512, 4, 8, 2048, 8192])):
         eng.set_precision(prec)
@@ -127,9 +127,10 @@ def test_product_library_rejects_untested_variants():
 
 
 def test_z_mix_epilogue_bit_identical():
-    """k_net_z's product epilogue (v_fma_mix for the lo part, the e4m3 Xh copy and the residual
-    seed) stores the same values as the unfused form (variant 2097152): logits and values of the
-    two builds must be bitwise equal, on an ordinary and on a wide-range net."""
+    """k_net_z's product epilogue (scaled conversions for the Xl8 / Xh8 copies and the residual
+    seed's decode, v_fma_mix for the exact differences) stores the same values as the unfused form
+    (variant 2097152) and as the round-2 form (v_fma_mix scalings, variant 33554432): logits and
+    values of the builds must be bitwise equal, on an ordinary and on a wide-range net."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from minitchess_alphazero_amd.network import Network
@@ -145,10 +146,11 @@ def test_z_mix_epilogue_bit_identical():
         pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=7)])
         eng.set_net_variant(0)
         l0, v0 = eng.evaluate(pos)
-        eng.set_net_variant(2097152)
-        l1, v1 = eng.evaluate(pos)
-        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
-        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+        for var in (2097152, 33554432):
+            eng.set_net_variant(var)
+            l1, v1 = eng.evaluate(pos)
+            assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), var
+            assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), var
 
 
 def test_z_loop_forms_bit_identical():
@@ -192,7 +194,7 @@ def _tiny_activation_net(scale=2.0 ** -20):
     return net.eval()
 
 
-@pytest.mark.parametrize('precision,var0,var1', [('f16f8', 0, 2097152), ('f16x3', 0, 1024)])
+@pytest.mark.parametrize('precision,var0,var1', [('f16f8', 0, 2097152), ('f16f8', 0, 33554432), ('f16x3', 0, 1024)])
 def test_mix_epilogue_bit_identical_tiny_activations(precision, var0, var1):
     """The v_fma_mix epilogues equal their unfused forms bitwise also when the activations are
     f16-subnormal (the mix path's exactness precondition)."""
