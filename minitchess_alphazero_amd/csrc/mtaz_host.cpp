@@ -1182,7 +1182,7 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
 // 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms,
 // 25165824 = the round-2 K loop (per-step fragment addresses, global-address weights; bit-identity
 // reference for the product's tap-major loop), 33554432 = the round-2 epilogue (unscaled
-// conversions), 67108864 = Wh fragments 3 steps ahead.  The
+// conversions), 58720256 = both (the round-2 product).  The
 // timing-only diagnostic builds (wrong results by construction) exist only in a library built
 // with MTAZ_NET_DIAG (tools/bench_net.py --diag).
 #ifdef MTAZ_NET_DIAG
@@ -1198,7 +1198,7 @@ extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   if (h->precision == NET_F16X3) ok = ok || variant == 1024;
   if (h->precision == NET_F16F8)
     ok = ok || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 || variant == 33554432 ||
-              variant == 67108864;
+              variant == 8388608 + 16777216 + 33554432;
 #ifdef MTAZ_NET_DIAG
   ok = true;
 #endif

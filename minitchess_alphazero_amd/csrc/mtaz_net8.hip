@@ -137,9 +137,8 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // offset recomputed per step and fragment), 16777216 = weights by 64-bit global addresses; all
   // four forms bit-identical (test_z_loop_forms_bit_identical).  31 -> 11 VALU and 17 -> 7 SALU
   // per step: -8.5% workgroup cycles, -5.7% launch time (profiles/r02_tap/).
-  // 67108864: Wh fragments 3 steps ahead instead of 1 (tap-major loop only)
-  constexpr bool PD3 = (VAR & 67108864) != 0;
-  constexpr int RA0 = (NW == 8 ? (PD3 ? 3 : 1) : 2) + 1;   // the A16 ring (PD + 1, below)
+  // (Wh fragments 3 steps ahead instead of 1: +0.7% time, 7 spilled registers; not kept)
+  constexpr int RA0 = (NW == 8 ? 1 : 2) + 1;   // the A16 ring (PD + 1, below)
   // (The e2m3 build spills some registers in either loop, 18 in the round-2 one and 23 in the
   // tap-major one, which is still 5% faster; with buffer-loaded weights it spills 30.)
   constexpr bool TAPA = (VAR & 8388608) == 0 && !DIAG_NOLDS && 8 % RA0 == 0;
@@ -870,7 +869,7 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
   if (var == 2097152) Z_LAUNCH(2097152, 512);
   else if (var == 8192) Z_LAUNCH(8192, 512);
   else if (var == 33554432) Z_LAUNCH(33554432, 512);
-  else if (var == 67108864) Z_LAUNCH(67108864, 512);
+  else if (var == 8388608 + 16777216 + 33554432) Z_LAUNCH(8388608 + 16777216 + 33554432, 512);
   else if (var == 8388608 + 16777216) Z_LAUNCH(8388608 + 16777216, 512);
 #ifdef MTAZ_NET_DIAG
   else if (var == 8388608) Z_LAUNCH(8388608, 512);

@@ -115,7 +115,7 @@ def test_product_library_rejects_untested_variants():
     from minitchess_alphazero_amd import _lib
     from minitchess_alphazero_amd.engine import Engine
     eng = Engine(n_games=4, sims=2)
-    for prec, good, bad in (('f16f8', [0, 8192, 2097152, 25165824, 33554432, 67108864],
+    for prec, good, bad in (('f16f8', [0, 8192, 2097152, 25165824, 33554432, 58720256],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
                             ('f16x3', [0, 1024], [512, 4, 8, 2048, 8192])):
         eng.set_precision(prec)
