@@ -100,8 +100,10 @@ class Engine:
     def set_net_variant(self, variant):
         """Select a parity-tested build of the current precision's network kernel (0 = product;
         set_precision resets it).  f16x3 (k_net_y): 1024 = the epilogue in unfused form.  f16f8
-        (k_net_z): 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross terms.  Other
-        values are rejected; the A/B and timing-only diagnostic builds exist only in
+        (k_net_z): 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross terms,
+        25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),
+        33554432 = the round-2 epilogue (unscaled conversions), 58720256 = both (the round-2
+        product); all but 8192 bitwise equal to 0.  Other values are rejected; the A/B and timing-only diagnostic builds exist only in
         libmtaz_diag.so (MTAZ_LIB, tools/bench_net.py --diag)."""
         _lib.check(self.L.mtaz_set_net_variant(self.h, int(variant)))
 
