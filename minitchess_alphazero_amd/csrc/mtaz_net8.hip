@@ -73,6 +73,24 @@ __device__ __forceinline__ uint32_t sc_fp8x4_f16(uint32_t h01, uint32_t h23, flo
   return __builtin_bit_cast(uint32_t, r);
 }
 
+// max over the wave's 64 lanes, in every lane: lanes i ^ 32 and i ^ 16 by gfx950's permlane
+// swaps, then row rotations by 8 and 4 and quad permutations by DPP (VALU only, instead of six
+// dependent ds_bpermute rounds through the LDS: epilogue share 8.1% -> 7.8% of the cycles,
+// profiles/r02_final/ab_wave_max_dpp.json); max is exact, so any order gives the same value
+__device__ __forceinline__ float wave_max_dpp(float x) {
+  uint32_t u = __float_as_uint(x);
+  const auto r32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  x = fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+  u = __float_as_uint(x);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  x = fmaxf(x, __uint_as_float(__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(x), 0x128, 0xf, 0xf, false)));
+  x = fmaxf(x, __uint_as_float(__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(x), 0x124, 0xf, 0xf, false)));
+  x = fmaxf(x, __uint_as_float(__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(x), 0x4e, 0xf, 0xf, false)));
+  x = fmaxf(x, __uint_as_float(__builtin_amdgcn_update_dpp(0, (int)__float_as_uint(x), 0xb1, 0xf, 0xf, false)));
+  return x;
+}
+
 // 4 e4m3 bytes of {a, b, c, d} (round to nearest even, OCP e4m3fn)
 __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d) {
   int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
@@ -191,8 +209,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   auto publish_max = [&](float* ymax, int xo) {
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) ymax[j] = fmaxf(ymax[j], __shfl_xor(ymax[j], o, 64));
+      ymax[j] = wave_max_dpp(ymax[j]);
     }
     if (lane < BPW) {
       float m = ymax[0];

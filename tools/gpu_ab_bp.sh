@@ -1,5 +1,5 @@
 #!/bin/bash
-# In-process A/B (diagnostic library): product vs the board-pair wave layout (4194304) on the
+# In-process A/B (diagnostic library): product vs a variant list (default: the board-pair wave layout 4194304) on the
 # tap-major loop.
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
