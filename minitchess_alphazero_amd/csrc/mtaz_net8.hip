@@ -156,7 +156,9 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // four forms bit-identical (test_z_loop_forms_bit_identical).  31 -> 11 VALU and 17 -> 7 SALU
   // per step: -8.5% workgroup cycles, -5.7% launch time (profiles/r02_tap/).
   // (Wh fragments 3 steps ahead instead of 1: +0.7% time, 7 spilled registers; not kept)
-  constexpr int RA0 = (NW == 8 ? 1 : 2) + 1;   // the A16 ring (PD + 1, below)
+  // the A16 ring (PD + 1, below): 2 with 8 waves; with 4 waves 4 in the tap-major loop, 3 in the
+  // round-2 one
+  constexpr int RA0 = NW == 8 ? 2 : (VAR & 8388608) ? 3 : 4;
   // (The e2m3 build spills some registers in either loop, 18 in the round-2 one and 23 in the
   // tap-major one, which is still 5% faster; with buffer-loaded weights it spills 30.)
   constexpr bool TAPA = (VAR & 8388608) == 0 && !DIAG_NOLDS && 8 % RA0 == 0;
