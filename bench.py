@@ -47,22 +47,45 @@ def _cpu_game(job):
     return {'seconds': st['seconds'], 'plies': st['plies'], 'nn_evals': st['nn_evals']}
 
 
-def cpu_baseline(plan, all_threads, gpu_sims):
-    """seeded games (np.random.seed(g), random-init weights) at C1's 32 sims and
-    at the GPU's sims per move, each on all cores (games one after another, torch.set_num_threads =
-    all_threads) and on 1 thread (all single-thread games at once, one process each: every game
-    still runs alone on one core).  Children are separate processes (spawned, never exec'ed over
-    this one) and touch no GPU.  value = games/s at the GPU's sims on all cores."""
+def host_cores():
+    """The host cores this process may use: os.cpu_count() (the whole machine), the affinity mask
+    and the cgroup CPU quota (the GPU box grants a share of a larger host).  'usable' = the
+    smaller of the last two: the thread count of the all-core CPU baseline."""
+    n_os = os.cpu_count() or 1
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = list(range(n_os))
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = len(aff) if quota is None else max(1, min(len(aff), int(quota)))
+    span = f'{aff[0]}-{aff[-1]}' if aff and aff[-1] - aff[0] + 1 == len(aff) else ','.join(map(str, aff))
+    return {'os_cpu_count': n_os, 'affinity_count': len(aff), 'affinity': span, 'cgroup_quota_cpus': quota,
+            'usable': usable}
+
+
+def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=()):
+    """seeded games (np.random.seed(g), random-init weights) at C1's 32 sims,
+    the repo's default 36 (app/base.py:25) and the GPU's sims per move, each on all cores (games one
+    after another, torch.set_num_threads = all_threads) and on 1 thread (all single-thread games at
+    once, one process each: every game still runs alone on one core).  Children are separate
+    processes (spawned, never exec'ed over this one) and touch no GPU.  value = games/s at the
+    GPU's sims on all cores."""
     import multiprocessing as mp
     seeds = [0, 1, 2] if plan == 'full' else [0]
-    sims_list = sorted({32, gpu_sims}) if plan == 'full' else [gpu_sims]
+    sims_list = sorted({32, gpu_sims, *extra_sims}) if plan == 'full' else sorted({gpu_sims, *extra_sims})
     ctx = mp.get_context('spawn')
     runs = {}
 
-    def record(sims, thr, games):
+    def record(sims, label, thr, games):
         secs = [g['seconds'] for g in games]
         log(f'cpu baseline {sims} sims, {thr} thread(s): {[round(x, 1) for x in secs]} s per game')
-        runs[f'{sims}sims/{"all" if thr == all_threads else thr}'] = {
+        runs[f'{sims}sims/{label}'] = {
             'threads': thr, 'seeds': seeds, 'seconds_per_game': [round(x, 3) for x in secs],
             'games_per_s': len(secs) / sum(secs), 'plies': [g['plies'] for g in games],
             'nn_evals': [g['nn_evals'] for g in games],
@@ -75,11 +98,12 @@ def cpu_baseline(plan, all_threads, gpu_sims):
         with ctx.Pool(len(jobs)) as pool:
             out = pool.map(_cpu_game, jobs, chunksize=1)
         for i, sims in enumerate(sims_list):
-            record(sims, 1, out[i * len(seeds):(i + 1) * len(seeds)])
+            record(sims, '1thread', 1, out[i * len(seeds):(i + 1) * len(seeds)])
     # all cores: the games one after another in one process
     for sims in sims_list:
         with ctx.Pool(1) as pool:
-            record(sims, all_threads, pool.map(_cpu_game, [(sims, sd, all_threads) for sd in seeds], chunksize=1))
+            record(sims, 'all', all_threads, pool.map(_cpu_game, [(sims, sd, all_threads) for sd in seeds],
+                                                      chunksize=1))
     head = runs[f'{gpu_sims}sims/all']
     return {'value': head['games_per_s'], 'unit': 'games/s', 'cores': all_threads, 'kind': 'port',
             'sample': (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
@@ -137,6 +161,10 @@ def main():
                          'quick: 1 game at --sims on all cores')
     ap.add_argument('--no-secondary', action='store_true',
                     help='skip the second timed step with the fp32-accurate k_net_y (f16x3)')
+    ap.add_argument('--default-sims', type=int, default=36,
+                    help="one more timed step at the repo's default sims per move (app/base.py:25: 36; 0 = skip), "
+                         'reported with its CPU baseline as at_repo_default_sims')
+    ap.add_argument('--no-memo', action='store_true', help='evaluate every leaf (Engine.set_memo(False))')
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
     ap.add_argument('--weights', default='', help='state_dict file (safetensors or torch.save) instead of random '
                                                   'init (BASELINE config 3: tests/golden/c3/c3.safetensors)')
@@ -191,17 +219,18 @@ def main():
             sd = load_file(args.weights)
         else:
             sd = torch.load(args.weights, map_location='cpu', weights_only=True)
-        net = Network()
-        net.load_state_dict(sd)
+        net_for_engine = Network()
+        net_for_engine.load_state_dict(sd)
         h = hashlib.sha256()                      # over the state_dict in module order (tests/golden/c3.json)
-        for k, v in net.state_dict().items():
+        for k, v in net_for_engine.state_dict().items():
             h.update(k.encode())
             h.update(v.detach().cpu().contiguous().numpy().tobytes())
         weights_sha = h.hexdigest()
-        eng.set_weights(net)
     else:
         torch.manual_seed(0)                      # random-init weights of the reference architecture
-        eng.set_weights(Network())
+        net_for_engine = Network()
+    eng.set_weights(net_for_engine)
+    eng.set_memo(not args.no_memo)
     eng.set_precision(args.precision)
     eng.set_net_variant(args.net_variant)
     eng.set_timing(True)
@@ -216,22 +245,40 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    tot = {'sims': 0.0, 'nn_evals': 0.0, 'plies': 0.0, 'trunk_ms': 0.0, 'trunk_boards': 0.0, 'waves': 0.0,
-           'terminal_sims': 0.0, 'decisive': 0.0, 'host_rng_ms': 0.0, 'sync_ms': 0.0, 'select_ms': 0.0,
-           'compact_ms': 0.0}
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        st = eng.play()
-        for k in tot:
-            tot[k] += st[k]
-        if rank == 0:
-            log(f'step {i + 1}/{args.steps}: {st["wall_ms"] / 1e3:.2f} s')
-    sync()
-    dt = time.perf_counter() - t0
-    dt, tot = reduce_run(dt, tot, dist, red_device)
+    KEYS = ('sims', 'nn_evals', 'memo_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
+            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms')
+
+    def timed(engine, steps, label):
+        """`steps` full self-play batches between barrier + synchronize; max wall over ranks and
+        summed counters (sharding.reduce_run)."""
+        tot = {k: 0.0 for k in KEYS}
+        sync()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            st = engine.play()
+            for k in tot:
+                tot[k] += st[k]
+            if rank == 0:
+                log(f'{label} step {i + 1}/{steps}: {st["wall_ms"] / 1e3:.2f} s')
+        sync()
+        dt = time.perf_counter() - t0
+        dt, tot = reduce_run(dt, tot, dist, red_device)
+        return dt, tot, int(st.get('net_precision', 0))
+
+    def counters(tot, dt, games):
+        ref_evals = tot['nn_evals'] + tot['memo_hits']
+        return {'sims_per_s': tot['sims'] / dt, 'plies_per_game': tot['plies'] / games,
+                # network evaluations: computed on the GPU, supplied by the per-game leaf memo, and their
+                # sum = the reference's evaluations (one per non-terminal expansion, exp/agent.py:64-71)
+                'nn_evals_per_game': tot['nn_evals'] / games, 'memo_hits_per_game': tot['memo_hits'] / games,
+                'nn_evals_reference_per_game': ref_evals / games,
+                'memo_hit_frac': tot['memo_hits'] / ref_evals if ref_evals else 0.0,
+                'nn_evals_per_s': tot['nn_evals'] / dt, 'nn_evals_reference_per_s': ref_evals / dt,
+                'terminal_sims_per_game': tot['terminal_sims'] / games, 'decisive_games': int(tot['decisive']),
+                'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12}
+
+    dt, tot, prec = timed(eng, args.steps, 'main')
     games = G * args.steps * world
-    prec = int(st.get('net_precision', 0))
 
     # secondary line: one more timed step on the fp32-accurate network (k_net_y, f16x3), same
     # engine, seeds and workload, so both precisions' throughput comes from the same run
@@ -239,19 +286,28 @@ def main():
     if not args.no_secondary and args.precision == 'f16f8':
         eng.set_precision('f16x3')
         eng.evaluate(np.stack([start_position()] * 8))    # load k_net_y's code object
-        sync()
-        t1 = time.perf_counter()
-        st2 = eng.play()
-        sync()
-        dt2 = time.perf_counter() - t1
-        tot2 = {k: st2[k] for k in tot}
-        dt2, tot2 = reduce_run(dt2, tot2, dist, red_device)
-        if rank == 0:
-            log(f'secondary (k_net_y) step: {dt2:.2f} s')
+        dt2, tot2, _ = timed(eng, 1, 'secondary (k_net_y)')
         eng.set_precision(args.precision)
         secondary = {'precision': 'f16x3 (fp16 hi/lo split, three f16 MFMA passes; fp32-accurate to ~1e-8)',
                      'value': G * world / dt2, 'unit': 'games/s', 'steps': 1, 'ms_per_step': dt2 * 1e3,
-                     'sims_per_s': tot2['sims'] / dt2, 'roofline': kernel_roofline(tot2, 1)}
+                     'roofline': kernel_roofline(tot2, 1), **counters(tot2, dt2, G * world)}
+
+    # the north_star's measurement point: the repo's default sims per move (app/base.py:25), same
+    # games, seeds, weights and precision as the main line
+    at_default = None
+    if args.default_sims and args.default_sims != sims:
+        eng36 = Engine(n_games=G, sims=args.default_sims, device=device, seed_base=seed_base)
+        eng36.set_weights(net_for_engine)
+        eng36.set_precision(args.precision)
+        eng36.set_net_variant(args.net_variant)
+        eng36.set_timing(True)
+        eng36.set_pipeline(args.groups)
+        eng36.set_memo(not args.no_memo)
+        eng36.evaluate(np.stack([start_position()] * 8))
+        dt3, tot3, prec3 = timed(eng36, 1, f'{args.default_sims} sims')
+        at_default = {'sims_per_move': args.default_sims, 'value': G * world / dt3, 'unit': 'games/s', 'steps': 1,
+                      'ms_per_step': dt3 * 1e3, 'roofline': kernel_roofline(tot3, prec3), **counters(tot3, dt3, G * world)}
+        eng36.close()
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -289,13 +345,7 @@ def main():
                                (f'{G} parallel self-play games per GPU, {sims} sims/move, trained checkpoint '
                                 f'(BASELINE config 3)'),
                    'games_per_gpu': G, 'sims_per_move': sims, 'parallelism': f'games sharded over {world} GPU(s)'},
-        'sims_per_s': tot['sims'] / dt,
-        'nn_evals_per_s': tot['nn_evals'] / dt,
-        'plies_per_game': tot['plies'] / games,
-        'nn_evals_per_game': tot['nn_evals'] / games,
-        'terminal_sims_per_game': tot['terminal_sims'] / games,
-        'decisive_games': int(tot['decisive']),
-        'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12,
+        **counters(tot, dt, games),
         'roofline': roof,
         # secondary roofline: the tree kernel k_select, HBM/latency-bound; algorithmic
         # bytes per simulation = SURVEY's estimate (path nodes: header + k edge reads + edge update,
@@ -316,10 +366,19 @@ def main():
     }
     if secondary is not None:
         line['secondary'] = secondary
+    if at_default is not None:
+        line['at_repo_default_sims'] = at_default
+    line['host_cores'] = host_cores()
     if world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line['cpu_baseline'] = cpu_baseline(args.cpu_plan, threads, sims)
+        threads = args.cpu_threads or line['host_cores']['usable']
+        extra = (args.default_sims,) if at_default is not None else ()
+        line['cpu_baseline'] = cpu_baseline(args.cpu_plan, threads, sims, extra)
         line['vs_cpu_baseline'] = line['value'] / line['cpu_baseline']['value']
+        if at_default is not None:
+            r36 = line['cpu_baseline']['runs'][f'{args.default_sims}sims/all']
+            at_default['cpu_baseline_games_per_s'] = r36['games_per_s']
+            at_default['cpu_baseline_sims_per_s'] = r36['sims_per_s']
+            at_default['vs_cpu_baseline'] = at_default['value'] / r36['games_per_s']
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define MTAZ_ABI_VERSION 1
+#define MTAZ_ABI_VERSION 2
 
 #define MTAZ_E_FAIL (-1)
 #define MTAZ_E_ILLEGAL (-2)     /* exp/environment.py:11 IlegalMoveException          */
@@ -137,6 +137,9 @@ int mtaz_set_timing(mtaz_engine* h, int on);
 int mtaz_set_precision(mtaz_engine* h, int precision);
 /* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
 int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
+/* host threads of the per-move work (Dirichlet draws, action choice; 0 = the CPUs of the process's
+ * affinity mask, at most 16).  Pipeline groups split them. */
+int mtaz_set_host_threads(mtaz_engine* h, int n);
 /* network-only timing harness: avg ms over `iters` launches on n device positions; with
  * stamped != 0 also per-workgroup [nwg][stem, conv K loops, epilogues, heads cycles, total
  * cycles, total 100 MHz ticks] from a separate diagnostic build (tools/bench_net.py) */
@@ -156,6 +159,21 @@ int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_agent1);
  * while another's network occupies the GPU.  Games keep their global seeds, so results are
  * identical for any group count.  Applies to full-batch mtaz_play(h, n_games, 0) only. */
 int mtaz_set_pipeline(mtaz_engine* h, int groups);
+/* Leaf memo (1 = per game, the default; 0 = off).  The reference evaluates its network on every
+ * leaf it expands (exp/agent.py:64-71), a pure function of the position; each of a game's two
+ * agents keeps its own table (app/base.py:113), so a position one agent expanded earlier is
+ * evaluated again when the other agent reaches it.  With the memo the second expansion copies the
+ * first one's legal list, priors and value (or terminal value) from the other table: every table,
+ * visit count and move is unchanged, the network runs on fewer leaves.  Off automatically when
+ * the agents use different weight slots (mtaz_set_agent_slots). */
+int mtaz_set_memo(mtaz_engine* h, int mode);
+/* Edge storage of the MCTS tables (exp/agent.py:29-36 keeps a list of Q/N/P per node; here a
+ * node's children are a contiguous edge range).  Each of the 2 * n_games tables owns a region of
+ * per_tree edges; a node whose children do not fit takes them from a pool of `pool` edges shared
+ * by all tables, so no single table's size is a limit, only the pool's exhaustion (then
+ * MTAZ_E_CAPACITY, "edge-capacity").  Defaults: 16 and 8 * n_games * 2 edges per node of a table.
+ * Reallocates and clears every table (between games only); pipeline groups keep the default. */
+int mtaz_set_edge_capacity(mtaz_engine* h, int64_t per_tree, int64_t pool);
 
 /* ---- fine-grained search (MonteCarloTreeSearch.simulate, exp/agent.py:41-45, and
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */
@@ -165,8 +183,10 @@ int mtaz_get_games(mtaz_engine* h, uint32_t* roots, int32_t* agents, uint8_t* ac
 int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n);
 /* root legal count and "root not yet visited" per game (decides the Dirichlet draws) */
 int mtaz_move_begin(mtaz_engine* h, int32_t* root_k, int32_t* root_new);
-/* Dirichlet vectors for this move: game g, draw j, child c at noise[offsets[g] + j*k + c] */
-int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, int64_t total);
+/* Dirichlet vectors for this move: game g, draw j, child c at noise[offsets[g] + j*strides[g] + c]
+ * (strides[g] = the root's legal count k; NULL = the counts of this move's mtaz_move_begin, an
+ * error without one since mtaz_create / mtaz_set_games) */
+int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, const int32_t* strides, int64_t total);
 /* run sims [first, first+n) with the GPU network as leaf evaluator */
 int mtaz_simulate(mtaz_engine* h, int first_sim, int n_sims);
 /* host-evaluator mode: select -> (get leaves, caller computes P and v) -> set -> backup */
@@ -185,10 +205,18 @@ int mtaz_sim_backup(mtaz_engine* h);
 int mtaz_move_end(mtaz_engine* h, uint16_t* codes, uint32_t* visits, int32_t* k, int kout);
 /* MinitChessEpisode.step for every active game + game-level result (with history) */
 int mtaz_apply(mtaz_engine* h, const int32_t* actions);
-/* read-only tree view for parity tests (mcts['N'|'Q'|'P'|'legal_moves'|'terminal']) */
+/* read-only tree view for parity tests (mcts['N'|'Q'|'P'|'legal_moves'|'terminal']): edges = the
+ * summed legal-list length of the non-terminal nodes; tree_get writes node i's children compactly
+ * at [e0[i], e0[i] + k[i]) of codes / P / Q / N, in node order */
 int mtaz_tree_size(mtaz_engine* h, int tree, int32_t* nodes, int32_t* edges);
 int mtaz_tree_get(mtaz_engine* h, int tree, uint32_t* pos, uint32_t* e0, uint16_t* k, uint8_t* term, double* tval,
                   uint16_t* codes, float* P, double* Q, uint32_t* N);
+/* load a table from the mtaz_tree_get layout (n nodes; the hash index and visit sums are rebuilt):
+ * moves a MonteCarloTreeSearch into a larger engine when a later simulate() asks for more
+ * simulations than its first (exp/agent.py:41-45 has no such limit) */
+int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* pos, const uint32_t* e0, const uint16_t* k,
+                  const uint8_t* term, const double* tval, const uint16_t* codes, const float* P, const double* Q,
+                  const uint32_t* N);
 
 #ifdef __cplusplus
 }

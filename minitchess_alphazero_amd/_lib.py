@@ -56,8 +56,11 @@ SIGNATURES = {
     'mtaz_set_timing': (c_int, [c_void_p, c_int]),
     'mtaz_set_precision': (c_int, [c_void_p, c_int]),
     'mtaz_set_seed_base': (c_int, [c_void_p, c_uint64]),
+    'mtaz_set_host_threads': (c_int, [c_void_p, c_int]),
     'mtaz_set_net_variant': (c_int, [c_void_p, c_int]),
     'mtaz_set_pipeline': (c_int, [c_void_p, c_int]),
+    'mtaz_set_memo': (c_int, [c_void_p, c_int]),
+    'mtaz_set_edge_capacity': (c_int, [c_void_p, c_int64, c_int64]),
     'mtaz_set_weights_slot': (c_int, [c_void_p, c_int, POINTER(c_void_p), P_i64, c_int]),
     'mtaz_set_agent_slots': (c_int, [c_void_p, c_int, c_int]),
     'mtaz_net_time': (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, P_f32, POINTER(c_uint64)]),
@@ -65,7 +68,7 @@ SIGNATURES = {
     'mtaz_get_games': (c_int, [c_void_p, P_u32, P_i32, P_u8, P_i32]),
     'mtaz_clear_trees': (c_int, [c_void_p, P_i32, c_int]),
     'mtaz_move_begin': (c_int, [c_void_p, P_i32, P_i32]),
-    'mtaz_set_noise': (c_int, [c_void_p, P_f64, P_i64, c_int64]),
+    'mtaz_set_noise': (c_int, [c_void_p, P_f64, P_i64, P_i32, c_int64]),
     'mtaz_simulate': (c_int, [c_void_p, c_int, c_int]),
     'mtaz_sim_select': (c_int, [c_void_p, c_int]),
     'mtaz_leaves_get': (c_int, [c_void_p, P_i32, P_u32, P_i32, P_i32, P_u16]),
@@ -77,6 +80,7 @@ SIGNATURES = {
     'mtaz_apply': (c_int, [c_void_p, P_i32]),
     'mtaz_tree_size': (c_int, [c_void_p, c_int, P_i32, P_i32]),
     'mtaz_tree_get': (c_int, [c_void_p, c_int, P_u32, P_u32, P_u16, P_u8, P_f64, P_u16, P_f32, P_f64, P_u32]),
+    'mtaz_tree_set': (c_int, [c_void_p, c_int, c_int, P_u32, P_u32, P_u16, P_u8, P_f64, P_u16, P_f32, P_f64, P_u32]),
 }
 
 
@@ -109,10 +113,23 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    check_fingerprint(L.mtaz_version().decode())
     if L.mtaz_load_codec(CODEC_PATH.encode()) != 0:
         raise MtazLibraryError('codec load failed: ' + L.mtaz_last_error().decode())
     _LIB = L
     return L
+
+
+def check_fingerprint(version):
+    """The library must be built from the sources next to it (build.py source_hash, compiled into
+    mtaz_version()); raises MtazLibraryError otherwise.  Skipped only where no sources exist."""
+    from . import build as _build
+    if not os.path.isdir(_build.CSRC):
+        return
+    want = _build.source_hash()
+    if not version.endswith('mtaz-src-sha256=' + want):
+        raise MtazLibraryError(f'{LIB_PATH} was not built from this tree ({version}; sources {want}): run '
+                               '`python -m minitchess_alphazero_amd.build`')
 
 
 def check(rc):

@@ -45,25 +45,31 @@ def _weights_key(model):
 class MonteCarloTreeSearch:
     """exp/agent.py:24-88 on the GPU: a one-game engine whose table 0 is this tree."""
 
-    def __init__(self, environment, model, cpuct, device=0, cast_mode=2):
+    def __init__(self, environment, model, cpuct, device=0, cast_mode=2, capacity=None):
         self._environment = environment
         self._model = model
         self._cpuct = cpuct
         self._device = device
         self._cast_mode = cast_mode
+        self._capacity = capacity     # simulations per move the engine is first sized for (None: the first call's)
         self._engine = None
         self._sims = None
         self._wkey = None
         self._view = None
 
     def _engine_for(self, n):
+        """The one-game engine, sized for n simulations per move.  A later call with more
+        simulations than the engine was sized for (the reference has no such limit,
+        exp/agent.py:41-45) moves the table into a larger engine (mtaz_tree_set)."""
         from .engine import Engine
-        if self._engine is None:
-            self._engine = Engine(n_games=1, sims=n, device=self._device, cpuct=self._cpuct, cast_mode=self._cast_mode)
-            self._engine.clear_trees()
-            self._sims = n
-        elif n > self._sims:
-            raise ValueError(f'this tree was sized for {self._sims} simulations per move, got {n}')
+        if self._engine is None or n > self._sims:
+            sims = max(n, self._capacity or 0)
+            eng = Engine(n_games=1, sims=sims, device=self._device, cpuct=self._cpuct, cast_mode=self._cast_mode)
+            eng.clear_trees()
+            if self._engine is not None:
+                eng.set_tree(0, self._engine.tree_arrays(0))
+                self._engine.close()
+            self._engine, self._sims, self._wkey = eng, sims, None
         key = _weights_key(self._model)
         if key != self._wkey:
             self._engine.set_weights(self._model)

@@ -6,7 +6,13 @@ RNG compiled with -ffp-contract=off, engine driver) and csrc/mtaz_wire.cpp (epis
 format).  The shared object lands next to this file so it travels to the GPU box with the repo
 snapshot.  build(diag=True) makes libmtaz_diag.so with -DMTAZ_NET_DIAG: the network kernels'
 A/B and timing-only variants (tools/bench_net.py --diag), never loaded by the product path.
+
+Build fingerprint: source_hash() is the sha256 of every file under csrc/, include/mtaz.h and the
+compile commands below.  It is compiled into the library (mtaz_version() ends in "src=<hash>"),
+build() rebuilds whenever the library does not carry the tree's hash (content, not mtimes), and
+_lib.lib() refuses a library whose hash differs from the sources next to it.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -36,14 +42,35 @@ def _hipcc():
             return c
 
 
+def source_hash():
+    """sha256 over the library's sources (every file in csrc/, include/mtaz.h) and compile flags."""
+    h = hashlib.sha256()
+    files = sorted(os.listdir(CSRC))
+    for name in files:
+        path = os.path.join(CSRC, name)
+        if os.path.isfile(path):
+            h.update(b'csrc/' + name.encode() + b'\0')
+            with open(path, 'rb') as f:
+                h.update(f.read())
+    with open(os.path.join(INCLUDE, 'mtaz.h'), 'rb') as f:
+        h.update(b'include/mtaz.h\0' + f.read())
+    h.update(repr((SOURCES, ARCH)).encode())
+    return h.hexdigest()
+
+
+def embedded_hash(path):
+    """The src=<hash> a built library carries (None if absent)."""
+    try:
+        with open(path, 'rb') as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(b'mtaz-src-sha256=')
+    return data[i + 16:i + 80].decode('ascii', 'replace') if i >= 0 else None
+
+
 def _stale(out):
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    deps = [os.path.join(CSRC, s) for s, _ in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
-    deps.append(os.path.join(INCLUDE, 'mtaz.h'))
-    deps.append(os.path.abspath(__file__))
-    return any(os.path.getmtime(d) > t for d in deps)
+    return embedded_hash(out) != source_hash()
 
 
 def build(force=False, verbose=True, diag=False):
@@ -52,12 +79,14 @@ def build(force=False, verbose=True, diag=False):
         return out
     os.makedirs(bdir, exist_ok=True)
     hipcc = _hipcc()
+    sha = source_hash()
     objs = []
     procs = []
     for src, flags in SOURCES:
         obj = os.path.join(bdir, src + '.o')
         cmd = [hipcc, '-x', 'hip', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-c',
-               os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function'] + flags
+               os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function',
+               f'-DMTAZ_SRC_SHA256="{sha}"'] + flags
         if diag:
             cmd.append('-DMTAZ_NET_DIAG')
         if verbose:

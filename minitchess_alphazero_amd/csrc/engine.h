@@ -26,11 +26,13 @@ enum ErrBits : int32_t {
 
 // A node's scalars in one 16-B record (one load per level of the descent)
 struct alignas(16) NodeHdr {
-  uint32_t e0;            // tree-local first edge
+  uint32_t e0;            // first edge (a global edge index: the tree's own region or the pool)
   uint32_t sumN;          // sum of child N (exact; numpy N.sum())
   uint32_t kt;            // bits 0..15: number of children (legal list length, duplicates
                           // kept); HDR_TERM: terminal (exp/agent.py:59-63)
-  float tval;             // stored terminal value (= -reward: -1 or -0, exact in float)
+  float tval;             // terminal: the stored value (= -reward: -1 or -0, exact in float);
+                          // otherwise the leaf value v the network returned (exp/agent.py:67,72),
+                          // kept for the per-game leaf memo (Params::memo)
 };
 constexpr uint32_t HDR_TERM = 1u << 16;
 __host__ __device__ __forceinline__ int hdr_k(const NodeHdr& h) { return (int)(h.kt & 0xffffu); }
@@ -40,7 +42,10 @@ __host__ __device__ __forceinline__ bool hdr_term(const NodeHdr& h) { return (h.
 // {Q, N, P, terminal, visited, legal_moves} keyed by FEN; here a node is the
 // packed Pos key in an open-addressing table, its children a contiguous edge
 // range (SoA: code u16, P f32, Q f64, N u32, child node).  Tree t owns nodes [t*NC, (t+1)*NC),
-// hash slots [t*HC, ...), edges [t*EC, ...).
+// hash slots [t*HC, ...) and the edge region [t*EC, (t+1)*EC).  A node's k edges go to its
+// tree's region while they fit, else to the shared edge pool [pool_base, pool_base + pool_cap)
+// (one atomicAdd per spilled node), so one tree outgrowing its region costs nothing; only an
+// exhausted pool is an error.  Edge indices (NodeHdr::e0, path edges) are global.
 struct Trees {
   Pos* node_pos;
   NodeHdr* node_hdr;
@@ -52,7 +57,9 @@ struct Trees {
   double* e_Q;
   uint32_t* e_N;
   uint32_t* e_child;      // the child's node index once the edge has been followed, else NONE
+  uint32_t* pool_used;    // [1] edges handed out from the pool
   int NC, HC, EC;
+  uint32_t pool_base, pool_cap;
 };
 
 struct Games {
@@ -90,6 +97,7 @@ struct Leaves {
   Pos* pos;               // [G]
   float* P;               // [G*KMAX] priors (softmax over the legal logits)
   float* v;               // [G]
+  uint8_t* ghit;          // [G] 1 when game g's simulation took its leaf from the memo
 };
 
 struct Params {
@@ -102,6 +110,12 @@ struct Params {
   const double* sqrt_tab; // sqrt(n) for n < sqrt_n (exactly what np.sqrt returns)
   int sqrt_n;
   int32_t* err;
+  // leaf memo (0 = off, 1 = per game): a position the game's other agent already expanded takes
+  // its legal list, priors and value from that agent's table instead of a network evaluation.
+  // The network is a pure function of the position (exp/agent.py:64-71 evaluates
+  // process_observation(fen) alone), so the tables, and every result, are those without the memo.
+  // Off when the two agents search with different networks (arena).
+  int memo;
 };
 
 struct Dev {
@@ -192,9 +206,10 @@ void launch_encode_batch(const Pos* pos, int n, uint8_t* tokens, float* clocks, 
 void launch_replay_put(const Pos* pos, const int32_t* k, const int64_t* e0, const uint16_t* codes,
                        const uint32_t* visits, const float* reward, int n, int64_t cap, int64_t head,
                        uint8_t* tokens, float* clocks, float* pi, float* reward_out, hipStream_t s);
-void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s);
+// all_trees: also empties the edge pool (a partial reset leaves the pool's edges allocated)
+void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, bool all_trees, hipStream_t s);
 void launch_move_begin(const Dev& d, hipStream_t s);
-// k_select + k_leaf_compact; count_log (optional, device) receives the leaf count, ev_mid
+// k_select + k_leaf_compact; count_log (optional, device) receives [leaf count, memo hits], ev_mid
 // (optional) is recorded between the two kernels
 void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log = nullptr, hipEvent_t ev_mid = nullptr);
 #ifdef MTAZ_NET_DIAG

@@ -278,10 +278,10 @@ __device__ uint32_t tree_insert(const Trees& T, int t, const Pos& p, uint32_t sl
 __device__ __forceinline__ void backup_path(const Trees& T, int t, const uint32_t* pn, const uint32_t* pe, int depth,
                                             double v, int lane) {
 #pragma clang fp contract(off)
-  const size_t eb = (size_t)t * T.EC, nbase = (size_t)t * T.NC;
+  const size_t nbase = (size_t)t * T.NC;
   for (int d = lane; d < depth; d += 64) {
     const double vd = ((depth - d) & 1) ? -v : v;
-    const size_t e = eb + pe[d];
+    const size_t e = pe[d];
     const uint32_t Ni = T.e_N[e];
     const double N = (double)Ni;
     const double Q = T.e_Q[e];
@@ -293,7 +293,7 @@ __device__ __forceinline__ void backup_path(const Trees& T, int t, const uint32_
   }
 }
 
-__global__ void k_reset_trees(Trees T, const int32_t* __restrict__ trees, int ntrees) {
+__global__ void k_reset_trees(Trees T, const int32_t* __restrict__ trees, int ntrees, int all_trees) {
   const int j = blockIdx.y;
   if (j >= ntrees) return;
   const int t = trees[j];
@@ -302,12 +302,13 @@ __global__ void k_reset_trees(Trees T, const int32_t* __restrict__ trees, int nt
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     T.n_nodes[t] = 0;
     T.n_edges[t] = 0;
+    if (all_trees && j == 0) *T.pool_used = 0;
   }
 }
 
-void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, hipStream_t s) {
+void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, bool all_trees, hipStream_t s) {
   if (ntrees <= 0) return;
-  hipLaunchKernelGGL(k_reset_trees, dim3(4, ntrees), dim3(256), 0, s, d.tr, trees, ntrees);
+  hipLaunchKernelGGL(k_reset_trees, dim3(4, ntrees), dim3(256), 0, s, d.tr, trees, ntrees, all_trees ? 1 : 0);
 }
 
 // Move start: does the agent's table already hold the root (exp/agent.py:57)?  The host
@@ -388,7 +389,10 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
   __shared__ LegalLds s_l;
   __shared__ RuleTables s_rt;
   const int g = blockIdx.x, lane = threadIdx.x;
-  if (lane == 0) D.lf.gnode[g] = NONE;
+  if (lane == 0) {
+    D.lf.gnode[g] = NONE;
+    D.lf.ghit[g] = 0;
+  }
   if (!D.gm.active[g]) return;
 #ifdef MTAZ_NET_DIAG
   unsigned long long sel_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -398,7 +402,8 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
   load_rules_lds(&s_rt);
   const Trees& T = D.tr;
   const int t = 2 * g + D.gm.agent[g];
-  const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
+  const size_t nbase = (size_t)t * T.NC;
+  const uint32_t ebase = (uint32_t)t * (uint32_t)T.EC;   // the tree's own edge region
   uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
   const uint32_t n_nodes = T.n_nodes[t], n_edges = T.n_edges[t];
@@ -422,48 +427,88 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
       SEL_T(1);
       if (n == NONE) {
         // ---- expansion (exp/agent.py:57-73) ----
-        const BB b = unpack(pos);
-        const int k = wave_legal(b, D.pr.flags, s_rt, s_l);
-        SEL_T(3);
-        if (k < 0) {
-          if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
-          return;
+        // Leaf memo (Params::memo): the game's other table may hold this position already; its
+        // legal list, terminal value or network priors and value are then those a fresh
+        // expansion would compute (rules and network are functions of the position alone), and
+        // the simulation backs up here instead of queueing a leaf.  Tree t ^ 1 is idle during
+        // tree t's search (the agents alternate by ply), so it is read without synchronisation.
+        uint32_t m = NONE;
+        NodeHdr mh{0u, 0u, 0u, 0.0f};
+        if (D.pr.memo) {
+          uint32_t s2;
+          m = tree_find(T, t ^ 1, pos, &s2);
+          if (m != NONE) mh = T.node_hdr[(size_t)(t ^ 1) * T.NC + m];
         }
-        const int oc = outcome(b, k, in_check(b, s_rt), D.pr.flags, D.pr.move_cap, 1, s_rt);
+        int k;
+        bool term;
+        float tv;   // terminal: -reward (-1 or -0); memo hit: the stored leaf value
+        if (m != NONE) {
+          k = hdr_k(mh);
+          term = hdr_term(mh);
+          tv = mh.tval;
+        } else {
+          const BB b = unpack(pos);
+          k = wave_legal(b, D.pr.flags, s_rt, s_l);
+          SEL_T(3);
+          if (k < 0) {
+            if (lane == 0) atomicOr(D.pr.err, ERR_KMAX);
+            return;
+          }
+          const int oc = outcome(b, k, in_check(b, s_rt), D.pr.flags, D.pr.move_cap, 1, s_rt);
+          term = oc != ONGOING;
+          tv = (oc == DECISIVE) ? -1.0f : -0.0f;
+        }
         SEL_T(4);
-        uint32_t nn = NONE;
+        uint32_t nn = NONE, ne0 = 0;
         if (lane == 0) {
           nn = tree_insert(T, t, pos, slot, n_nodes, D.pr.err);
-          if (nn != NONE && oc == ONGOING && n_edges + (uint32_t)k > (uint32_t)T.EC) {
-            atomicOr(D.pr.err, ERR_EDGES);
-            nn = NONE;
+          if (nn != NONE && !term) {
+            if (n_edges + (uint32_t)k <= (uint32_t)T.EC) {   // the tree's own region
+              ne0 = ebase + n_edges;
+              T.n_edges[t] = n_edges + k;
+            } else {                                          // spill to the shared pool
+              const uint32_t q = atomicAdd(T.pool_used, (uint32_t)k);
+              if (q + (uint32_t)k <= T.pool_cap) {
+                ne0 = T.pool_base + q;
+              } else {
+                atomicOr(D.pr.err, ERR_EDGES);
+                nn = NONE;
+              }
+            }
           }
           if (nn != NONE) {
-            if (oc != ONGOING) {
-              T.node_hdr[nbase + nn] = NodeHdr{0u, 0u, HDR_TERM, (oc == DECISIVE) ? -1.0f : -0.0f};   // -reward
+            if (term) {
+              T.node_hdr[nbase + nn] = NodeHdr{0u, 0u, HDR_TERM, tv};
             } else {
-              T.n_edges[t] = n_edges + k;
-              T.node_hdr[nbase + nn] = NodeHdr{n_edges, 0u, (uint32_t)k, 0.0f};
-              D.lf.gnode[g] = nn;
-              D.lf.gpos[g] = pos;
-              D.gm.path_len[g] = depth;
+              T.node_hdr[nbase + nn] = NodeHdr{ne0, 0u, (uint32_t)k, m != NONE ? tv : 0.0f};
+              if (m == NONE) {
+                D.lf.gnode[g] = nn;
+                D.lf.gpos[g] = pos;
+                D.gm.path_len[g] = depth;
+              } else {
+                D.lf.ghit[g] = 1;
+              }
             }
-            if (pedge != NONE) T.e_child[ebase + pedge] = nn;
+            if (pedge != NONE) T.e_child[pedge] = nn;
             else D.gm.root_node[g] = nn;
           }
         }
         nn = __shfl(nn, 0, 64);
+        ne0 = __shfl(ne0, 0, 64);
         if (nn != NONE) {
-          if (oc == ONGOING) {
+          if (!term) {
+            const size_t msrc = mh.e0;
             for (int c = lane; c < k; c += 64) {
-              T.e_code[ebase + n_edges + c] = s_l.sorted[c];
-              T.e_P[ebase + n_edges + c] = 0.f;
-              T.e_Q[ebase + n_edges + c] = 0.0;
-              T.e_N[ebase + n_edges + c] = 0;
-              T.e_child[ebase + n_edges + c] = NONE;
+              const size_t e = (size_t)ne0 + c;
+              T.e_code[e] = m != NONE ? T.e_code[msrc + c] : s_l.sorted[c];
+              T.e_P[e] = m != NONE ? T.e_P[msrc + c] : 0.f;
+              T.e_Q[e] = 0.0;
+              T.e_N[e] = 0;
+              T.e_child[e] = NONE;
             }
+            if (m != NONE) backup_path(T, t, pn, pe, depth, (double)tv, lane);   // exp/agent.py:72
           } else {
-            backup_path(T, t, pn, pe, depth, (oc == DECISIVE) ? -1.0 : -0.0, lane);
+            backup_path(T, t, pn, pe, depth, (double)tv, lane);                  // exp/agent.py:59-63
           }
         }
         SEL_T(5);
@@ -472,7 +517,7 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
       }
       // found by lookup (a transposition, or the root without a valid hint): link it
       if (lane == 0) {
-        if (pedge != NONE) T.e_child[ebase + pedge] = n;
+        if (pedge != NONE) T.e_child[pedge] = n;
         else D.gm.root_node[g] = n;
       }
     }
@@ -504,7 +549,7 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
     uint32_t best_cc = 0;   // winner's code | linked child (the child index in a second word)
     uint32_t best_ch = NONE;
     for (int c = lane; c < k; c += 64) {
-      const size_t e = ebase + e0 + c;
+      const size_t e = (size_t)e0 + c;
       const float Pf = T.e_P[e];
       const double Q = T.e_Q[e];
       const double N = (double)T.e_N[e];
@@ -553,12 +598,14 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
 // The leaf batch in game order: one workgroup; per chunk of 4,096 games thread i holds games
 // 4i..4i+3 in registers (their leaf, agent and position in one round of loads: loads placed after
 // the stores would wait for them), a block scan of the per-thread counts places its leaves.
-// Also logs the count (count_log, when given).
+// Also logs the count and the number of memo hits (count_log[0..1], when given).
 __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restrict__ count_log) {
   constexpr int PER = 4;
   __shared__ int s_w[16];
+  __shared__ int s_hits;
   const int G = D.pr.G, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int base = 0;
+  if (tid == 0) s_hits = 0;
+  int base = 0, hits = 0;
   for (int c0 = 0; c0 < G; c0 += 1024 * PER) {
     const int g0 = c0 + tid * PER;
     uint32_t nd[PER];
@@ -571,6 +618,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
       nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
       ag[j] = in ? D.gm.agent[g0 + j] : 0;
       ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
+      hits += in ? (int)D.lf.ghit[g0 + j] : 0;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) c += nd[j] != NONE;
@@ -598,9 +646,15 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     }
     base += tot;
   }
+  for (int o = 32; o > 0; o >>= 1) hits += __shfl_xor(hits, o, 64);
+  if (lane == 0 && hits) atomicAdd(&s_hits, hits);
+  __syncthreads();
   if (tid == 0) {
     *D.lf.count = base;
-    if (count_log) *count_log = base;
+    if (count_log) {
+      count_log[0] = base;
+      count_log[1] = s_hits;
+    }
   }
 }
 
@@ -636,10 +690,11 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
   const Trees& T = D.tr;
   const int g = D.lf.game[i], t = D.lf.tree[i];
   const uint32_t n = D.lf.node[i];
-  const size_t nbase = (size_t)t * T.NC, ebase = (size_t)t * T.EC;
+  const size_t nbase = (size_t)t * T.NC;
   const NodeHdr hd = T.node_hdr[nbase + n];
   const int k = hdr_k(hd);
-  for (int c = lane; c < k; c += 64) T.e_P[ebase + hd.e0 + c] = D.lf.P[(size_t)i * KMAX + c];
+  for (int c = lane; c < k; c += 64) T.e_P[(size_t)hd.e0 + c] = D.lf.P[(size_t)i * KMAX + c];
+  if (lane == 0) T.node_hdr[nbase + n].tval = D.lf.v[i];   // kept for the leaf memo (Params::memo)
   const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
   backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i], lane);
@@ -658,7 +713,7 @@ __global__ void k_gather_leaf_codes(Dev D, uint16_t* __restrict__ codes, int32_t
   const NodeHdr hd = T.node_hdr[(size_t)t * T.NC + n];
   const int k = hdr_k(hd);
   const uint32_t e0 = hd.e0;
-  for (int c = threadIdx.x; c < k; c += blockDim.x) codes[(size_t)i * KMAX + c] = T.e_code[(size_t)t * T.EC + e0 + c];
+  for (int c = threadIdx.x; c < k; c += blockDim.x) codes[(size_t)i * KMAX + c] = T.e_code[(size_t)e0 + c];
   if (threadIdx.x == 0) kout[i] = k;
 }
 
@@ -686,8 +741,8 @@ __global__ __launch_bounds__(64) void k_move_end(Dev D, uint16_t* __restrict__ c
     return;
   }
   for (int c = lane; c < k; c += 64) {
-    codes[(size_t)g * kout + c] = T.e_code[(size_t)t * T.EC + e0 + c];
-    visits[(size_t)g * kout + c] = T.e_N[(size_t)t * T.EC + e0 + c];
+    codes[(size_t)g * kout + c] = T.e_code[(size_t)e0 + c];
+    visits[(size_t)g * kout + c] = T.e_N[(size_t)e0 + c];
   }
 }
 
@@ -943,7 +998,7 @@ __global__ __launch_bounds__(256) void k_heads(Dev D, NetWeights W, const float*
     const int t = D.lf.tree[b];
     const uint32_t n = D.lf.node[b];
     const uint32_t e0 = D.tr.node_hdr[(size_t)t * D.tr.NC + n].e0;
-    for (int c = tid; c < sk; c += 256) scode[c] = D.tr.e_code[(size_t)t * D.tr.EC + e0 + c];
+    for (int c = tid; c < sk; c += 256) scode[c] = D.tr.e_code[(size_t)e0 + c];
   }
   if (tid < 90) {
     const int o = tid / 30, p = tid - o * 30;

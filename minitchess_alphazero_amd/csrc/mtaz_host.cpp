@@ -20,7 +20,9 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <sched.h>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mtaz.h"
@@ -47,7 +49,11 @@ static int set_err(int code, const char* fmt, ...) {
   } while (0)
 
 extern "C" int mtaz_abi_version(void) { return MTAZ_ABI_VERSION; }
-extern "C" const char* mtaz_version(void) { return "mtaz 0.1 (gfx950)"; }
+#ifndef MTAZ_SRC_SHA256
+#define MTAZ_SRC_SHA256 "unknown"
+#endif
+// the build fingerprint (build.py source_hash: csrc/*, include/mtaz.h, compile flags)
+extern "C" const char* mtaz_version(void) { return "mtaz 0.3 (gfx950) mtaz-src-sha256=" MTAZ_SRC_SHA256; }
 extern "C" const char* mtaz_last_error(void) { return g_err.c_str(); }
 
 // ---------------------------------------------------------------------------------------
@@ -444,7 +450,7 @@ struct PlyRec {
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
-  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_COUNT
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_COUNT
 };
 
 // Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
@@ -514,18 +520,32 @@ class HostPool {
   bool stop_ = false;
 };
 
+// The host threads this process may use: the CPUs of its affinity mask (not the machine's count:
+// one rank per GPU runs on its own slice of the host, launch.py / bench.py pin them), at most 16.
+int default_host_threads() {
+  cpu_set_t cs;
+  int n = 0;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+  if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 16));
+}
+
+// One pool per calling thread (the main thread, or each stream group's thread) for every
+// parallel_for, rebuilt only when the requested size changes.
+HostPool* host_pool(int nt) {
+  thread_local std::unique_ptr<HostPool> pool;
+  if (!pool || pool->size() != nt) pool.reset(new HostPool(nt));
+  return pool.get();
+}
+
 template <class F>
-void parallel_for(int n, F f) {
-  int nt = (int)std::thread::hardware_concurrency();
-  nt = std::max(1, std::min(nt, 16));
-  if (n < 64 || nt == 1) {
+void parallel_for(int n, int nt, F f) {
+  if (n < 64 || nt <= 1) {
     for (int i = 0; i < n; ++i) f(i);
     return;
   }
-  thread_local std::unique_ptr<HostPool> pool;
-  if (!pool) pool.reset(new HostPool(nt));
   const std::function<void(int)> fn = [&f](int i) { f(i); };
-  pool->run(n, fn);
+  host_pool(nt)->run(n, fn);
 }
 
 double now_ms() {
@@ -576,6 +596,7 @@ struct mtaz_engine {
   float* wxinv = nullptr;
   float* wyrange = nullptr;
   std::vector<void*> allocs;
+  std::vector<void*> edge_allocs;       // the edge arrays (alloc_edges; mtaz_set_edge_capacity replaces them)
   float* wbuf = nullptr;
   // scratch
   int32_t* d_actions = nullptr;
@@ -601,6 +622,7 @@ struct mtaz_engine {
   int wave = 0;
   int groups = 1;                       // mtaz_set_pipeline
   std::vector<mtaz_engine*> parts;      // per-group engines (borrow this engine's weights)
+  std::unique_ptr<HostPool> group_pool; // one persistent host thread per group (play_groups)
   // two-network play (arena, exp/learner.py:97-145): weight slot 0 / 1; the active slot's
   // buffers are the fields above (w, wbuf, wxbuf, wxinv, wyrange, weights_ok), the other
   // slot's are parked here; agent_slot maps agent 0 (first mover) / agent 1 to a slot
@@ -614,13 +636,18 @@ struct mtaz_engine {
   } parked;
   int cur_slot = 0;
   int agent_slot[2] = {0, 0};
+  int memo = 1;                         // leaf memo mode (mtaz_set_memo; Params::memo)
+  int host_threads = default_host_threads();   // per-move host work (mtaz_set_host_threads)
 
   ~mtaz_engine() {
+    group_pool.reset();
     for (mtaz_engine* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     if (noise_host) (void)hipHostFree(noise_host);
     for (auto e : ev) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
+    for (void* p : edge_allocs) (void)hipFree(p);
+    if (d.gm.noise) (void)hipFree(d.gm.noise);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -641,6 +668,50 @@ struct mtaz_engine {
     if (e_ < 0) return e_; \
   } while (0)
 
+// Edge arrays: T regions of `ec` edges (one per tree) followed by a shared pool of `pool` edges
+// (Trees).  Edge indices are u32, so T * ec + pool must stay below 2^32.
+static int alloc_edges(mtaz_engine* h, int64_t ec, int64_t pool) {
+  Trees& tr = h->d.tr;
+  const int64_t T = 2 * (int64_t)h->G;
+  if (ec < 1 || pool < 0 || T * ec + pool >= (int64_t)NONE)
+    return set_err(MTAZ_E_CAPACITY, "edge capacity %lld per tree x %lld trees + pool %lld exceeds 32-bit edge indices",
+                   (long long)ec, (long long)T, (long long)pool);
+  for (void* p : h->edge_allocs) (void)hipFree(p);
+  h->edge_allocs.clear();
+  const size_t TE = (size_t)(T * ec + pool);
+  auto grab = [&](auto** p, size_t elt) -> int {
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, std::max<size_t>(TE * elt, 16)));
+    h->edge_allocs.push_back(q);
+    *p = (std::remove_reference_t<decltype(*p)>)q;
+    return 0;
+  };
+  ECHK(grab(&tr.e_code, 2));
+  ECHK(grab(&tr.e_P, 4));
+  ECHK(grab(&tr.e_Q, 8));
+  ECHK(grab(&tr.e_N, 4));
+  ECHK(grab(&tr.e_child, 4));
+  tr.EC = (int)ec;
+  tr.pool_base = (uint32_t)(T * ec);
+  tr.pool_cap = (uint32_t)pool;
+  HIPCHK(hipMemset(tr.pool_used, 0, 4));
+  HIPCHK(hipMemset(tr.n_edges, 0, T * 4));
+  return 0;
+}
+
+// the device buffer of a move's Dirichlet draws, grown geometrically (the old buffer is freed:
+// callers have synchronised the stream, nothing reads it any more)
+static int ensure_noise(mtaz_engine* h, size_t n) {
+  if (n <= h->noise_cap && h->d.gm.noise) return 0;
+  const size_t cap = std::max(n, 2 * h->noise_cap);
+  if (h->d.gm.noise) HIPCHK(hipFree(h->d.gm.noise));
+  h->d.gm.noise = nullptr;
+  h->noise_cap = 0;
+  HIPCHK(hipMalloc(&h->d.gm.noise, cap * 8));
+  h->noise_cap = cap;
+  return 0;
+}
+
 static int engine_alloc(mtaz_engine* h) {
   const int G = h->G, T = 2 * G;
   Trees& tr = h->d.tr;
@@ -651,23 +722,26 @@ static int engine_alloc(mtaz_engine* h) {
   int hc = 1;
   while (hc < 2 * tr.NC) hc <<= 1;
   tr.HC = hc;
-  tr.EC = tr.NC * 24;   // average legal moves per expanded node <= 24 (trained nets reach 16+ at 256 sims)
   gm.DMAX = 2 * max_moves + 8;
   gm.HMAX = 2 * max_moves + 8;
-  const size_t TN = (size_t)T * tr.NC, TE = (size_t)T * tr.EC;
+  const size_t TN = (size_t)T * tr.NC;
   ECHK(h->dalloc(&tr.node_pos, TN));
   ECHK(h->dalloc(&tr.node_hdr, TN));
   ECHK(h->dalloc(&tr.hash, (size_t)T * tr.HC));
   ECHK(h->dalloc(&tr.n_nodes, T));
   ECHK(h->dalloc(&tr.n_edges, T));
-  ECHK(h->dalloc(&tr.e_code, TE));
-  ECHK(h->dalloc(&tr.e_P, TE));
-  ECHK(h->dalloc(&tr.e_Q, TE));
-  ECHK(h->dalloc(&tr.e_N, TE));
-  ECHK(h->dalloc(&tr.e_child, TE));
+  ECHK(h->dalloc(&tr.pool_used, 1));
   HIPCHK(hipMemset(tr.hash, 0, (size_t)T * tr.HC * 4));
   HIPCHK(hipMemset(tr.n_nodes, 0, T * 4));
-  HIPCHK(hipMemset(tr.n_edges, 0, T * 4));
+  // edges: 16 per node in each tree's region (random-init games average ~7.5 legal moves per
+  // node, the C3 net ~11) plus a shared pool of 8 per node per tree for the trees that outgrow
+  // theirs (a C3 game at 256 sims reached 16+ per node), capped by the 32-bit edge index
+  {
+    int64_t ec = 16 * (int64_t)tr.NC, pool = 8 * (int64_t)tr.NC * T;
+    const int64_t lim = (int64_t)NONE - 1;
+    if ((int64_t)T * ec + pool > lim) pool = std::max<int64_t>(0, lim - (int64_t)T * ec);
+    ECHK(alloc_edges(h, ec, pool));
+  }
   ECHK(h->dalloc(&gm.root, G));
   ECHK(h->dalloc(&gm.root_node, G));
   HIPCHK(hipMemset(gm.root_node, 0xff, G * 4));
@@ -687,8 +761,7 @@ static int engine_alloc(mtaz_engine* h) {
   HIPCHK(hipMemset(gm.agent, 0, G * 4));
   HIPCHK(hipMemset(gm.nhist, 0, G * 4));
   HIPCHK(hipMemset(gm.outcome, 0, G * 4));
-  h->noise_cap = (size_t)G * h->sims * 16;
-  ECHK(h->dalloc(&gm.noise, h->noise_cap));
+  ECHK(ensure_noise(h, (size_t)G * h->sims * 16));
   ECHK(h->dalloc(&lf.gnode, G));
   ECHK(h->dalloc(&lf.gpos, G));
   ECHK(h->dalloc(&lf.count, 1));
@@ -698,14 +771,16 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&lf.pos, G));
   ECHK(h->dalloc(&lf.P, (size_t)G * KMAX));
   ECHK(h->dalloc(&lf.v, G));
+  ECHK(h->dalloc(&lf.ghit, G));
+  HIPCHK(hipMemset(lf.ghit, 0, G));
   ECHK(h->dalloc(&h->d_actions, G));
   ECHK(h->dalloc(&h->d_root_codes, (size_t)G * KMAX));
   ECHK(h->dalloc(&h->d_root_visits, (size_t)G * KMAX));
   ECHK(h->dalloc(&h->d_leaf_codes, (size_t)G * KMAX));
   ECHK(h->dalloc(&h->d_leaf_k, G));
   ECHK(h->dalloc(&h->d_trees, T));
-  h->count_log_cap = h->sims * (2 * max_moves + 8);
-  ECHK(h->dalloc(&h->d_count_log, h->count_log_cap));
+  h->count_log_cap = h->sims * (2 * max_moves + 8);   // waves; two ints each (leaves, memo hits)
+  ECHK(h->dalloc(&h->d_count_log, 2 * (size_t)h->count_log_cap));
   // exact sqrt(N.sum()) table: N.sum() <= sims * searches per agent
   const int sqn = tr.NC + 2;
   std::vector<double> sq(sqn);
@@ -724,6 +799,7 @@ static int engine_alloc(mtaz_engine* h) {
   pr.move_cap = h->move_cap;
   pr.sqrt_tab = h->d_sqrt;
   pr.sqrt_n = sqn;
+  pr.memo = h->memo;
   // network activations: [G][256][32] x 3
   h->nb.B = G;
   ECHK(h->dalloc(&h->nb.x0, (size_t)G * 8192));
@@ -1232,10 +1308,22 @@ extern "C" int mtaz_set_weights_slot(mtaz_engine* h, int slot, const float* cons
   return rc;
 }
 
+// the memo shares leaf results between a game's two tables: only when both agents search with the
+// same network
+static void sync_memo(mtaz_engine* h) { h->d.pr.memo = h->agent_slot[0] == h->agent_slot[1] ? h->memo : 0; }
+
 extern "C" int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_agent1) {
   if ((slot_agent0 | slot_agent1) & ~1) return set_err(MTAZ_E_FAIL, "weight slots must be 0 or 1");
   h->agent_slot[0] = slot_agent0;
   h->agent_slot[1] = slot_agent1;
+  sync_memo(h);
+  return 0;
+}
+
+extern "C" int mtaz_set_memo(mtaz_engine* h, int mode) {
+  if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "memo mode must be 0 (off) or 1 (per game)");
+  h->memo = mode;
+  sync_memo(h);
   return 0;
 }
 
@@ -1246,6 +1334,12 @@ extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
     h->parts.clear();
   }
   h->groups = groups;
+  return 0;
+}
+
+extern "C" int mtaz_set_host_threads(mtaz_engine* h, int n) {
+  if (n < 0) return set_err(MTAZ_E_FAIL, "host thread count must be >= 0");
+  h->host_threads = n ? n : default_host_threads();
   return 0;
 }
 
@@ -1293,6 +1387,7 @@ extern "C" int mtaz_set_games(mtaz_engine* h, const uint32_t* roots, const int32
   HIPCHK(hipMemcpyAsync(h->d.gm.nhist, zero.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.outcome, zero.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  h->last_root_k.clear();   // new roots: the next mtaz_set_noise needs a fresh mtaz_move_begin or strides
   return 0;
 }
 
@@ -1319,7 +1414,7 @@ extern "C" int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n) {
   for (int i = 0; i < n; ++i)
     if (trees[i] < 0 || trees[i] >= 2 * h->G) return set_err(MTAZ_E_FAIL, "tree index %d out of range", trees[i]);
   HIPCHK(hipMemcpyAsync(h->d_trees, trees, n * 4, hipMemcpyHostToDevice, h->stream));
-  launch_reset_trees(h->d, h->d_trees, n, h->stream);
+  launch_reset_trees(h->d, h->d_trees, n, !all.empty(), h->stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
@@ -1336,21 +1431,23 @@ extern "C" int mtaz_move_begin(mtaz_engine* h, int32_t* root_k, int32_t* root_ne
   return rc;
 }
 
-extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, int64_t total) {
+extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t* offsets, const int32_t* strides,
+                              int64_t total) {
   HIPCHK(hipSetDevice(h->device));
-  if ((size_t)total > h->noise_cap) {
-    // grow (rare: long legal lists)
-    void* q = nullptr;
-    HIPCHK(hipMalloc(&q, total * 8));
-    h->allocs.push_back(q);
-    h->d.gm.noise = (double*)q;
-    h->noise_cap = total;
+  // per-game contiguous draws: the draw stride of game g is its vector length, the root's legal
+  // count: strides[g], or (strides NULL) the counts of this move's mtaz_move_begin
+  std::vector<int32_t> js(h->G, 0);
+  if (strides) {
+    for (int g = 0; g < h->G; ++g) js[g] = strides[g];
+  } else {
+    if ((int)h->last_root_k.size() != h->G)
+      return set_err(MTAZ_E_FAIL, "mtaz_set_noise without strides needs mtaz_move_begin first");
+    js = h->last_root_k;
   }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  ECHK(ensure_noise(h, (size_t)std::max<int64_t>(total, 1)));
   if (total > 0) HIPCHK(hipMemcpyAsync(h->d.gm.noise, noise, total * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offsets, h->G * 8, hipMemcpyHostToDevice, h->stream));
-  // per-game contiguous draws: draw stride = the game's root legal count (mtaz_move_begin)
-  std::vector<int32_t> js(h->G, 0);
-  for (int g = 0; g < h->G && g < (int)h->last_root_k.size(); ++g) js[g] = h->last_root_k[g];
   HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
@@ -1372,7 +1469,7 @@ static int sim_gpu(mtaz_engine* h, int sim) {
     eb = h->ev[4 * h->wave + 2];
     ee = h->ev[4 * h->wave + 3];
   }
-  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + h->wave : nullptr, em);
+  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + 2 * (size_t)h->wave : nullptr, em);
   launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, eb, ee);
   launch_backup(h->d, h->stream);
   HIPCHK(hipGetLastError());
@@ -1469,34 +1566,122 @@ extern "C" int mtaz_apply(mtaz_engine* h, const int32_t* actions) {
   return check_err(h);
 }
 
-extern "C" int mtaz_tree_size(mtaz_engine* h, int tree, int32_t* nodes, int32_t* edges) {
+static int read_tree_headers(mtaz_engine* h, int tree, std::vector<NodeHdr>& hd) {
   if (tree < 0 || tree >= 2 * h->G) return set_err(MTAZ_E_FAIL, "tree out of range");
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemcpy(nodes, h->d.tr.n_nodes + tree, 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(edges, h->d.tr.n_edges + tree, 4, hipMemcpyDeviceToHost));
+  int32_t nn = 0;
+  HIPCHK(hipMemcpy(&nn, h->d.tr.n_nodes + tree, 4, hipMemcpyDeviceToHost));
+  hd.resize(nn);
+  if (nn) HIPCHK(hipMemcpy(hd.data(), h->d.tr.node_hdr + (size_t)tree * h->d.tr.NC, nn * sizeof(NodeHdr), hipMemcpyDeviceToHost));
   return 0;
 }
 
+// edges = the summed legal-list length of the tree's expanded (non-terminal) nodes
+extern "C" int mtaz_tree_size(mtaz_engine* h, int tree, int32_t* nodes, int32_t* edges) {
+  std::vector<NodeHdr> hd;
+  ECHK(read_tree_headers(h, tree, hd));
+  int64_t ne = 0;
+  for (const NodeHdr& x : hd)
+    if (!hdr_term(x)) ne += hdr_k(x);
+  *nodes = (int32_t)hd.size();
+  *edges = (int32_t)ne;
+  return 0;
+}
+
+// Node i's children are written at [e0[i], e0[i] + k[i]) of the output arrays, node after node
+// (the device places them in the tree's region or the shared pool; this view is compact).
 extern "C" int mtaz_tree_get(mtaz_engine* h, int tree, uint32_t* pos, uint32_t* e0, uint16_t* k, uint8_t* term,
                              double* tval, uint16_t* codes, float* P, double* Q, uint32_t* N) {
-  int32_t nn = 0, ne = 0;
-  ECHK(mtaz_tree_size(h, tree, &nn, &ne));
+  std::vector<NodeHdr> hd;
+  ECHK(read_tree_headers(h, tree, hd));
+  const int nn = (int)hd.size();
   const Trees& T = h->d.tr;
-  const size_t nb = (size_t)tree * T.NC, eb = (size_t)tree * T.EC;
-  HIPCHK(hipMemcpy(pos, T.node_pos + nb, nn * sizeof(Pos), hipMemcpyDeviceToHost));
-  std::vector<NodeHdr> hd(nn);
-  HIPCHK(hipMemcpy(hd.data(), T.node_hdr + nb, nn * sizeof(NodeHdr), hipMemcpyDeviceToHost));
+  if (nn) HIPCHK(hipMemcpy(pos, T.node_pos + (size_t)tree * T.NC, nn * sizeof(Pos), hipMemcpyDeviceToHost));
+  uint32_t o = 0;
   for (int i = 0; i < nn; ++i) {
-    e0[i] = hd[i].e0;
+    const int kk = hdr_term(hd[i]) ? 0 : hdr_k(hd[i]);
+    e0[i] = o;
     k[i] = (uint16_t)hdr_k(hd[i]);
     term[i] = hdr_term(hd[i]) ? 1 : 0;
     tval[i] = (double)hd[i].tval;
+    if (kk) {
+      const size_t s = hd[i].e0;
+      HIPCHK(hipMemcpy(codes + o, T.e_code + s, kk * 2, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(P + o, T.e_P + s, kk * 4, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(Q + o, T.e_Q + s, kk * 8, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(N + o, T.e_N + s, kk * 4, hipMemcpyDeviceToHost));
+    }
+    o += kk;
   }
-  HIPCHK(hipMemcpy(codes, T.e_code + eb, ne * 2, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(P, T.e_P + eb, ne * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(Q, T.e_Q + eb, ne * 8, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(N, T.e_N + eb, ne * 4, hipMemcpyDeviceToHost));
   return nn;
+}
+
+// Load table `tree` from the mtaz_tree_get layout (nodes in order; node i's children at
+// [e0[i], e0[i] + k[i]) of codes / P / Q / N for non-terminal nodes).  The hash index, the visit
+// sums and the node headers are rebuilt; child links start unset (k_select relinks them by lookup).
+extern "C" int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* pos, const uint32_t* e0,
+                             const uint16_t* k, const uint8_t* term, const double* tval, const uint16_t* codes,
+                             const float* P, const double* Q, const uint32_t* N) {
+  if (tree < 0 || tree >= 2 * h->G) return set_err(MTAZ_E_FAIL, "tree out of range");
+  Trees& T = h->d.tr;
+  if (n < 0 || n > T.NC) return set_err(MTAZ_E_CAPACITY, "%d nodes do not fit a table of %d", n, T.NC);
+  HIPCHK(hipSetDevice(h->device));
+  std::vector<Pos> np(n);
+  std::vector<NodeHdr> hd(n);
+  std::vector<uint32_t> hash(T.HC, 0u);
+  const uint32_t ebase = (uint32_t)tree * (uint32_t)T.EC;
+  int64_t ne = 0;
+  for (int i = 0; i < n; ++i) {
+    np[i] = pos_in(pos + 5 * i);
+    uint32_t s = pos_hash(np[i]) & (uint32_t)(T.HC - 1);
+    while (hash[s]) s = (s + 1) & (uint32_t)(T.HC - 1);
+    hash[s] = (uint32_t)i + 1;
+    if (term[i]) {
+      hd[i] = NodeHdr{0u, 0u, HDR_TERM, (float)tval[i]};
+      continue;
+    }
+    uint64_t sum = 0;
+    for (int c = 0; c < k[i]; ++c) sum += N[e0[i] + c];
+    hd[i] = NodeHdr{ebase + (uint32_t)ne, (uint32_t)sum, (uint32_t)k[i], (float)tval[i]};
+    ne += k[i];
+  }
+  if (ne > T.EC) return set_err(MTAZ_E_CAPACITY, "%lld edges do not fit a table region of %d", (long long)ne, T.EC);
+  std::vector<uint16_t> ec(ne);
+  std::vector<float> ep(ne);
+  std::vector<double> eq(ne);
+  std::vector<uint32_t> en(ne), ech(ne, NONE);
+  for (int i = 0, o = 0; i < n; ++i) {
+    if (term[i]) continue;
+    for (int c = 0; c < k[i]; ++c, ++o) {
+      ec[o] = codes[e0[i] + c];
+      ep[o] = P[e0[i] + c];
+      eq[o] = Q[e0[i] + c];
+      en[o] = N[e0[i] + c];
+    }
+  }
+  const uint32_t nn32 = (uint32_t)n, ne32 = (uint32_t)ne;
+  HIPCHK(hipMemcpy(T.node_pos + (size_t)tree * T.NC, np.data(), n * sizeof(Pos), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.node_hdr + (size_t)tree * T.NC, hd.data(), n * sizeof(NodeHdr), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.hash + (size_t)tree * T.HC, hash.data(), (size_t)T.HC * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.n_nodes + tree, &nn32, 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(T.n_edges + tree, &ne32, 4, hipMemcpyHostToDevice));
+  if (ne) {
+    HIPCHK(hipMemcpy(T.e_code + ebase, ec.data(), ne * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_P + ebase, ep.data(), ne * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_Q + ebase, eq.data(), ne * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_N + ebase, en.data(), ne * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_child + ebase, ech.data(), ne * 4, hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+extern "C" int mtaz_set_edge_capacity(mtaz_engine* h, int64_t per_tree, int64_t pool) {
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (mtaz_engine* p : h->parts) delete p;   // groups re-create their engines with the default
+  h->parts.clear();
+  ECHK(alloc_edges(h, per_tree, pool));
+  return mtaz_clear_trees(h, nullptr, 0);
 }
 
 extern "C" int mtaz_set_timing(mtaz_engine* h, int on) {
@@ -1530,18 +1715,21 @@ static int play_groups(mtaz_engine* h) {
     p->precision = h->precision;
     p->variant = h->variant;
     p->timing = h->timing;
+    p->host_threads = std::max(1, h->host_threads / ng);   // the groups share this engine's threads
+    p->memo = h->memo;
+    sync_memo(p);
     p->seed_base = h->seed_base + (uint64_t)i * Gp;
   }
   std::vector<int> rc(ng, 0);
   std::vector<std::string> err(ng);
-  std::vector<std::thread> th;
   const double t0 = now_ms();
-  for (int i = 0; i < ng; ++i)
-    th.emplace_back([&, i]() {
-      rc[i] = mtaz_play(h->parts[i], Gp, 0);
-      if (rc[i] < 0) err[i] = mtaz_last_error();
-    });
-  for (auto& t : th) t.join();
+  // the group threads (and the host pools they own) persist across plays
+  if (!h->group_pool || h->group_pool->size() != ng) h->group_pool.reset(new HostPool(ng));
+  const std::function<void(int)> body = [&](int i) {
+    rc[i] = mtaz_play(h->parts[i], Gp, 0);
+    if (rc[i] < 0) err[i] = mtaz_last_error();
+  };
+  h->group_pool->run(ng, body);
   for (int i = 0; i < ng; ++i)
     if (rc[i] < 0) return set_err(rc[i], "group %d: %s", i, err[i].c_str());
   h->rec.clear();
@@ -1637,13 +1825,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
       if (active[g]) K += root_k[g];
     }
     const size_t need = (size_t)std::max<int64_t>(K, 1) * h->sims;
-    if (need > h->noise_cap) {
-      void* q = nullptr;
-      HIPCHK(hipMalloc(&q, need * 8));
-      h->allocs.push_back(q);
-      h->d.gm.noise = (double*)q;
-      h->noise_cap = need;
-    }
+    ECHK(ensure_noise(h, need));   // (mtaz_move_begin synchronised the stream)
     if (need > h->noise_host_cap) {
       if (h->noise_host) HIPCHK(hipHostFree(h->noise_host));
       HIPCHK(hipHostMalloc(&h->noise_host, need * 8, hipHostMallocDefault));
@@ -1658,7 +1840,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     auto chunk_end = [&](int j0) { return std::min(j0 == 0 ? 1 : j0 + NCH, h->sims); };
     auto draw_chunk = [&](int j0) {   // draws [j0, chunk_end(j0)) of every active game
       const int je = chunk_end(j0);
-      parallel_for(G, [&](int g) {
+      parallel_for(G, h->host_threads, [&](int g) {
         if (!active[g]) return;
         const int k = root_k[g], jn = std::min(je, h->sims - root_new[g]);
         for (int j = j0; j < jn; ++j) legacy_dirichlet(h->rng[g], h->alpha, k, h->noise_host + (size_t)j * K + offs[g]);
@@ -1688,7 +1870,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     sync_ms += now_ms() - ts;
     // action selection (exp/agent.py:110-119) + records (exp/callbacks.py:40-47)
     tr = now_ms();
-    parallel_for(G, [&](int g) {
+    parallel_for(G, h->host_threads, [&](int g) {
       if (!active[g]) return;
       const int k = root_k[g];
       const uint16_t* c = codes.data() + (size_t)g * kmx;
@@ -1728,11 +1910,15 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   if (two_nets) activate_slot(h, 0);
   for (int g = 0; g < G; ++g) h->final_outcome[g] = outcome_v[g];
   // stats
-  std::vector<int32_t> counts(std::min(h->wave, h->count_log_cap));
-  if (!counts.empty())
-    HIPCHK(hipMemcpy(counts.data(), h->d_count_log, counts.size() * 4, hipMemcpyDeviceToHost));
-  double evals = 0;
-  for (int c : counts) evals += c;
+  const int nlog = std::min(h->wave, h->count_log_cap);
+  std::vector<int32_t> clog(2 * (size_t)nlog), counts(nlog);
+  if (nlog) HIPCHK(hipMemcpy(clog.data(), h->d_count_log, clog.size() * 4, hipMemcpyDeviceToHost));
+  double evals = 0, hits = 0;
+  for (int wv = 0; wv < nlog; ++wv) {
+    counts[wv] = clog[2 * wv];
+    evals += clog[2 * wv];
+    hits += clog[2 * wv + 1];
+  }
   double trunk_ms = 0, trunk_boards = 0, select_ms = 0, compact_ms = 0;
   if (h->timing) {
     for (int wv = 0; wv < h->wave && wv < (int)counts.size(); ++wv) {
@@ -1760,8 +1946,9 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (size_t t = 0; t < nn.size(); ++t) mxn = std::max(mxn, nn[t]), mxe = std::max(mxe, ne[t]);
   }
   h->stats[ST_PLIES] = (double)plies;
-  h->stats[ST_NN_EVALS] = evals;
-  h->stats[ST_TERMINAL_SIMS] = h->stats[ST_SIMS] - evals;
+  h->stats[ST_NN_EVALS] = evals;                              // network evaluations computed
+  h->stats[ST_MEMO_HITS] = hits;                              // leaves the memo supplied
+  h->stats[ST_TERMINAL_SIMS] = h->stats[ST_SIMS] - evals - hits;
   h->stats[ST_TRUNK_MS] = trunk_ms;
   h->stats[ST_TRUNK_BOARDS] = trunk_boards;
   h->stats[ST_WAVES] = h->wave;
@@ -1773,6 +1960,11 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_TRUNK_LAUNCHES] = h->timing ? 18.0 * h->wave : 0;
   h->stats[ST_MAX_NODES] = mxn;
   h->stats[ST_MAX_EDGES] = mxe;
+  {
+    uint32_t pu = 0;
+    HIPCHK(hipMemcpy(&pu, h->d.tr.pool_used, 4, hipMemcpyDeviceToHost));
+    h->stats[ST_POOL_EDGES] = pu;
+  }
   h->stats[ST_SYNC_MS] = sync_ms;
   h->stats[ST_NET_PREC] = h->precision;
   h->stats[ST_SELECT_MS] = select_ms;
@@ -1783,6 +1975,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
 extern "C" int mtaz_stats(mtaz_engine* h, double* out, int n) {
   h->stats[ST_NODE_CAP] = h->d.tr.NC;   // per-table capacities (engine_alloc)
   h->stats[ST_EDGE_CAP] = h->d.tr.EC;
+  h->stats[ST_POOL_CAP] = h->d.tr.pool_cap;
   for (int i = 0; i < n && i < ST_COUNT; ++i) out[i] = h->stats[i];
   return ST_COUNT;
 }

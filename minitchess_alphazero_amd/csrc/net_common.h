@@ -211,7 +211,7 @@ __device__ __forceinline__ void heads_out(const Dev& D, char* smem, int b0, int 
   const NodeHdr hd = D.tr.node_hdr[(size_t)t * D.tr.NC + n];
   const int k = hdr_k(hd);
   const uint32_t e0 = hd.e0;
-  const uint16_t* codes = D.tr.e_code + (size_t)t * D.tr.EC + e0;
+  const uint16_t* codes = D.tr.e_code + e0;
   float lg[KMAX / 64];
   float mx = -__builtin_inff();
 #pragma unroll

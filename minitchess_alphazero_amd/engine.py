@@ -24,7 +24,7 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
-              'select_ms', 'node_cap', 'edge_cap', 'compact_ms']
+              'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
@@ -111,6 +111,23 @@ class Engine:
         """play() over `groups` independent game groups on their own HIP streams (1 = off).
         Results are identical for any group count (games keep their global seeds)."""
         _lib.check(self.L.mtaz_set_pipeline(self.h, int(groups)))
+
+    def set_memo(self, on=True):
+        """Leaf memo (default on): a position the game's other agent already expanded takes its
+        legal list, priors and value from that agent's table instead of the network (results
+        unchanged; include/mtaz.h mtaz_set_memo).  stats()['nn_evals'] counts the evaluations
+        computed, 'memo_hits' the ones the memo supplied; their sum is the reference's count."""
+        _lib.check(self.L.mtaz_set_memo(self.h, 1 if on else 0))
+
+    def set_edge_capacity(self, per_tree, pool):
+        """Edge storage: `per_tree` edges in each table's own region plus a pool of `pool` edges
+        shared by the tables that outgrow theirs (include/mtaz.h mtaz_set_edge_capacity).  Clears
+        every table."""
+        _lib.check(self.L.mtaz_set_edge_capacity(self.h, int(per_tree), int(pool)))
+
+    def set_host_threads(self, n=0):
+        """Host threads of the per-move work (0 = the process's affinity mask, at most 16)."""
+        _lib.check(self.L.mtaz_set_host_threads(self.h, int(n)))
 
     def set_seed_base(self, seed_base):
         """Game slot g of the next play() uses np.random.seed(seed_base + g) semantics."""
@@ -206,16 +223,18 @@ class Engine:
     def set_noise(self, per_game):
         """per_game[g] = float64 array [draws, k] (or None) -> packed upload."""
         offs = np.zeros(self.G, np.int64)
+        strides = np.zeros(self.G, np.int32)
         chunks, total = [], 0
         for g in range(self.G):
             offs[g] = total
             a = per_game[g] if g < len(per_game) else None
             if a is not None and np.size(a):
-                a = np.ascontiguousarray(a, np.float64).reshape(-1)
-                chunks.append(a)
+                a = np.ascontiguousarray(a, np.float64)
+                strides[g] = a.shape[-1]                  # vector length = the root's legal count
+                chunks.append(a.reshape(-1))
                 total += a.size
         flat = np.concatenate(chunks) if chunks else np.zeros(1, np.float64)
-        _lib.check(self.L.mtaz_set_noise(self.h, _p(flat, c_double), _p(offs, c_int64), total))
+        _lib.check(self.L.mtaz_set_noise(self.h, _p(flat, c_double), _p(offs, c_int64), _p(strides, c_int32), total))
 
     def simulate(self, first_sim, n_sims):
         _lib.check(self.L.mtaz_simulate(self.h, int(first_sim), int(n_sims)))
@@ -270,6 +289,31 @@ class Engine:
         a = np.zeros(self.G, np.int32)
         a[:len(actions)] = actions
         _lib.check(self.L.mtaz_apply(self.h, _p(a, c_int32)))
+
+    def tree_arrays(self, t):
+        """Table t = 2*game + agent as arrays (mtaz_tree_get): pos [n,5], e0, k, term, tval per node;
+        codes, P, Q, N per edge, node i's children at [e0[i], e0[i] + k[i])."""
+        nn, ne = c_int32(), c_int32()
+        _lib.check(self.L.mtaz_tree_size(self.h, int(t), ctypes.byref(nn), ctypes.byref(ne)))
+        n, e = nn.value, ne.value
+        a = {'pos': np.zeros((max(n, 1), 5), np.uint32), 'e0': np.zeros(max(n, 1), np.uint32),
+             'k': np.zeros(max(n, 1), np.uint16), 'term': np.zeros(max(n, 1), np.uint8),
+             'tval': np.zeros(max(n, 1), np.float64), 'codes': np.zeros(max(e, 1), np.uint16),
+             'P': np.zeros(max(e, 1), np.float32), 'Q': np.zeros(max(e, 1), np.float64),
+             'N': np.zeros(max(e, 1), np.uint32)}
+        _lib.check(self.L.mtaz_tree_get(self.h, int(t), _p(a['pos'], c_uint32), _p(a['e0'], c_uint32),
+                                        _p(a['k'], c_uint16), _p(a['term'], c_uint8), _p(a['tval'], c_double),
+                                        _p(a['codes'], c_uint16), _p(a['P'], c_float), _p(a['Q'], c_double),
+                                        _p(a['N'], c_uint32)))
+        a['n'] = n
+        return a
+
+    def set_tree(self, t, a):
+        """Load table t from tree_arrays() output (possibly of another engine)."""
+        _lib.check(self.L.mtaz_tree_set(self.h, int(t), int(a['n']), _p(a['pos'], c_uint32), _p(a['e0'], c_uint32),
+                                        _p(a['k'], c_uint16), _p(a['term'], c_uint8), _p(a['tval'], c_double),
+                                        _p(a['codes'], c_uint16), _p(a['P'], c_float), _p(a['Q'], c_double),
+                                        _p(a['N'], c_uint32)))
 
     def tree(self, t):
         """Read-only view of table t = 2*game + agent in the reference's MCTS data layout:

@@ -200,6 +200,31 @@ class ReplayBuffer:
         self.size = min(self.cap, self.size + n)
         self.head = (self.head + over) % self.cap
 
+    def push_rows(self, rows):
+        """Append dict rows (InfoRecorder format, the MQTT learner's push_data) in order: tokens and
+        clock by the HIP encoder, pi by dense_pi (exp/learner.py:29-30), written to the slots after
+        the newest row like push_records, so both push paths share one ring in arrival order."""
+        n = len(rows)
+        if n == 0:
+            return
+        if n > self.max_length:
+            rows, n = rows[n - self.max_length:], self.max_length
+        dev = self.device
+        pos = np.stack([pos_from_fen(r['observation']) for r in rows])
+        tok, clk = encode_positions(pos, dev)
+        pi = torch.from_numpy(dense_pi(rows)).to(dev)
+        rew = torch.tensor([float(r['reward']) for r in rows], dtype=torch.float32, device=dev)
+        if self.size + n > self.cap and self.cap < self.max_length:
+            self._alloc(min(self.max_length, max(2 * self.cap, self.size + n)))
+        slots = (torch.arange(n, device=dev) + self.head + self.size) % self.cap
+        self._tokens[slots] = tok.reshape(n, 60).to(torch.uint8)
+        self._clock[slots] = clk.reshape(n)
+        self._pi[slots] = pi
+        self._reward[slots] = rew
+        over = max(0, self.size + n - self.cap)
+        self.size = min(self.cap, self.size + n)
+        self.head = (self.head + over) % self.cap
+
     def gather(self, i):
         """Rows i (device index tensor, 0 = oldest) -> (pi, tokens [.,2,6,5] i64, clock [.,1],
         reward [.,1]); capturable in a HIP graph (head is fixed for an update)."""
@@ -240,13 +265,16 @@ class EpisodeRecords:
     def __len__(self):
         return int(self.k.shape[0])
 
+    def slice(self, a, b):
+        """Rows [a, b)."""
+        e0, e1 = int(self.k[:a].sum()), int(self.k[:b].sum())
+        return EpisodeRecords(self.pos[a:b], self.k[a:b], self.codes[e0:e1], self.visits[e0:e1], self.reward[a:b])
+
     def tail(self, n):
         """The last n rows (deque(maxlen) semantics of exp/dataset.py:8)."""
         if n >= len(self):
             return self
-        start = len(self) - n
-        e0 = int(self.k[:start].sum())
-        return EpisodeRecords(self.pos[start:], self.k[start:], self.codes[e0:], self.visits[e0:], self.reward[start:])
+        return self.slice(len(self) - n, len(self))
 
     def pi_dense(self):
         """[N, 554] float32 targets, the same values and duplicate rule as dense_pi(rows)."""
@@ -430,7 +458,9 @@ class LearnPuppet:
     def _init_dataset(self):
         self._dataset = SimpleAlphaZeroDataset(max_length=self._max_length)
         self._records = EpisodeRecords.concat([])
-        self._arrivals = []          # ('rows', list of dicts) / ('records', EpisodeRecords), in push order
+        # host learner only: ('rows', list of dicts) / ('records', EpisodeRecords) in push order, for
+        # an update over both push paths (a GPU learner puts both into the HBM ring in push order)
+        self._arrivals = []
         if getattr(self, '_replay', None) is not None:
             self._replay.clear()
 
@@ -461,24 +491,34 @@ class LearnPuppet:
     def simulate(self):
         self._status = MasterOfPuppetsStatus.SIMULATE
 
+    def _ring(self):
+        if self._learner._device.type != 'cuda':
+            return None
+        if self._replay is None:
+            self._replay = ReplayBuffer(self._max_length, self._learner._device)
+        return self._replay
+
     def push_data(self, data):
         """One episode's rows (app/learner.py:54 -> app/base.py:182-185)."""
         if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
             self._episode_counter += 1
             self._dataset.push(data)
-            self._arrivals.append(('rows', data))
+            ring = self._ring()
+            if ring is not None:
+                ring.push_rows(list(data))
+            else:
+                self._arrivals.append(('rows', data))
 
     def push_records(self, records, episodes):
         """push_data for packed rows (EpisodeRecords) of `episodes` episodes.  On a GPU learner
         the rows go straight into the HBM replay ring (ReplayBuffer), encoded on arrival."""
         if MasterOfPuppetsStatus[self.status] == MasterOfPuppetsStatus.SIMULATE:
             self._episode_counter += episodes
-            self._arrivals.append(('records', records))
-            if self._learner._device.type == 'cuda':
-                if self._replay is None:
-                    self._replay = ReplayBuffer(self._max_length, self._learner._device)
-                self._replay.push_records(records)
+            ring = self._ring()
+            if ring is not None:
+                ring.push_records(records)
             else:
+                self._arrivals.append(('records', records))
                 self._records = EpisodeRecords.concat([self._records, records]).tail(self._max_length)
 
     def update(self, encode=True):

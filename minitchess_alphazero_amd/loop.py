@@ -89,8 +89,10 @@ def arena_round(new_net, old_net, games, sims, dist, device, seed_base):
 
 
 def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None, device=0, seed=0,
-             log=print, arena_games=0, gate_threshold=0.55):
-    """C5 on this node.  Returns rank 0's per-iteration history (other ranks: [])."""
+             log=print, arena_games=0, gate_threshold=0.55, on_iteration=None):
+    """C5 on this node.  Returns rank 0's per-iteration history (other ranks: []).
+    on_iteration(it, net, records, history_entry), rank 0 only, after the weights of
+    iteration `it` are in place (tools/train_stress.py measures the network there)."""
     from .engine import Engine
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
@@ -149,6 +151,8 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
                  'plies_per_game': st['plies'] / games}
             if verdict is not None:
                 h['arena'] = verdict
+            if on_iteration is not None:
+                on_iteration(it, net, EpisodeRecords.concat(parts), h)
             history.append(h)
             log(json.dumps(h))
     return history, net

@@ -27,7 +27,18 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
         assert s in _lib.SIGNATURES, f'{s} missing from the ctypes signature table'
-    assert L.mtaz_abi_version() == 1
+    assert L.mtaz_abi_version() == 2
+
+
+def test_library_carries_the_tree_fingerprint():
+    """The loaded library was built from these sources (build.py source_hash is compiled into
+    mtaz_version); a library from other sources is refused."""
+    from minitchess_alphazero_amd import build
+    ver = _lib.lib().mtaz_version().decode()
+    assert ver.endswith('mtaz-src-sha256=' + build.source_hash())
+    assert build.embedded_hash(_lib.LIB_PATH) == build.source_hash()
+    with pytest.raises(_lib.MtazLibraryError):
+        _lib.check_fingerprint(ver[:-64] + '0' * 64)
 
 
 def test_codec_file_matches_reference_hash():

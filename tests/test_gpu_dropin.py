@@ -69,6 +69,35 @@ def test_mcts_view_matches_reference_layout():
     assert m['N'][STARTING_FEN].sum() == 31
 
 
+def test_mcts_grows_for_more_simulations():
+    """A later simulate() may ask for more simulations than the first (exp/agent.py:41-45 has no
+    limit): the table moves into a larger engine (mtaz_tree_set) and the search continues exactly
+    as in a tree sized for the larger count from the start."""
+    import torch
+    from minitchess_alphazero_amd.agent import MonteCarloTreeSearch
+    from minitchess_alphazero_amd.environment import MinitChessEnvironment, STARTING_FEN, pos_step, pos_from_fen, pos_to_fen
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    fen2 = pos_to_fen(pos_step(pos_from_fen(STARTING_FEN), int(MinitChessEnvironment().new_episode()[0].get_legal_moves()[0])))
+    views = []
+    for cap in (None, 40):
+        m = MonteCarloTreeSearch(MinitChessEnvironment(), net, 1, capacity=cap)
+        np.random.seed(5)
+        m.simulate(8, STARTING_FEN)
+        m.simulate(40, fen2)                       # regrows when capacity is None
+        m.simulate(24, STARTING_FEN)
+        st = np.random.get_state()
+        views.append((m._data, (st[1].tobytes(), st[2])))
+    (a, pa), (b, pb) = views
+    assert pa == pb                                # same np.random consumption
+    assert a['visited'] == b['visited'] and a['terminal'] == b['terminal']
+    for fen in b['Q']:
+        assert a['legal_moves'][fen] == b['legal_moves'][fen]
+        assert np.array_equal(a['N'][fen], b['N'][fen]) and np.array_equal(a['Q'][fen], b['Q'][fen]), fen
+        assert np.array_equal(a['P'][fen], b['P'][fen]), fen
+
+
 def test_puppet_publishes_reference_payloads():
     from minitchess_alphazero_amd import puppet as pp
 

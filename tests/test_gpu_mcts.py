@@ -36,18 +36,28 @@ def test_select_expand_backup_synthetic_vs_reference_traces():
             assert [r['reward'] for r in got] == [r['reward'] for r in gm['moves']]
 
 
-def test_trees_bit_exact_vs_oracle():
-    """Final transposition tables (Q, N, P, legal_moves, terminal, visited) equal the oracle's."""
+@pytest.mark.parametrize('memo,spill', [(True, False), (False, False), (True, True)],
+                         ids=['memo', 'no-memo', 'memo-pool-spill'])
+def test_trees_bit_exact_vs_oracle(memo, spill):
+    """Final transposition tables (Q, N, P, legal_moves, terminal, visited) equal the oracle's,
+    with the per-game leaf memo (the default) and without it, and with table regions of 40 edges
+    so that most nodes take their children from the shared edge pool.  The host evaluator sees
+    every leaf the engine asks for: all of the oracle's expansions without the memo, fewer with it."""
     from oracle.mcts import SyntheticEvaluator
     from oracle import selfplay
     ev = SyntheticEvaluator(salt=3)
     seeds = [101, 102, 103]
     eng = _engine(len(seeds), 24)
+    eng.set_memo(memo)
+    if spill:
+        eng.set_edge_capacity(40, 1 << 20)
     trees = []
-    recs, _ = drive_engine(eng, len(seeds), 24, seeds, evaluator=ev, trees_out=trees)
+    recs, dst = drive_engine(eng, len(seeds), 24, seeds, evaluator=ev, trees_out=trees)
+    ref_evals = 0
     for g, s in enumerate(seeds):
         st = {}
         ref = selfplay.play_games(ev, 1, 24, seed_base=s, stats=st)[0]
+        ref_evals += st['nn_evals']
         assert compare_records(recs[g], ref)[2] is None
         for agent in (0, 1):
             mine, theirs = trees[g][agent], st['trees'][0][agent]
@@ -59,6 +69,61 @@ def test_trees_bit_exact_vs_oracle():
                 assert np.array_equal(mine['Q'][fen], theirs['Q'][fen]), fen
                 assert np.array_equal(mine['N'][fen], theirs['N'][fen]), fen
                 assert np.array_equal(mine['P'][fen], np.asarray(theirs['P'][fen], np.float32)), fen
+    if memo:
+        assert dst['nn_evals'] < ref_evals
+    else:
+        assert dst['nn_evals'] == ref_evals
+
+
+def test_leaf_memo_leaves_games_unchanged():
+    """The leaf memo changes which leaves the network evaluates, not the games: with the GPU network,
+    memo on and off give identical records, and computed + memo-supplied evaluations equal the
+    evaluations without the memo (the reference's count: one per non-terminal expansion)."""
+    import torch
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    out = {}
+    for memo in (True, False):
+        eng = _engine(32, 16, seed_base=11)
+        eng.set_weights(net)
+        eng.set_memo(memo)
+        out[memo] = (eng.play(), eng.records())
+    (st_on, r_on), (st_off, r_off) = out[True], out[False]
+    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+        assert np.array_equal(r_on[key], r_off[key]), key
+    assert st_off['memo_hits'] == 0 and st_on['memo_hits'] > 0
+    assert st_on['nn_evals'] + st_on['memo_hits'] == st_off['nn_evals']
+    assert st_on['terminal_sims'] == st_off['terminal_sims']
+    print(f"memo: {st_on['memo_hits']:.0f} of {st_off['nn_evals']:.0f} evaluations supplied "
+          f"({st_on['memo_hits'] / st_off['nn_evals']:.1%})")
+
+
+def test_edge_pool_spill_and_exhaustion():
+    """Tables that outgrow their edge region continue in the shared pool with unchanged games; an
+    exhausted pool fails the call with the edge-capacity flag (exp/agent.py:64-66 never fails, so
+    the pool is sized from memory, 8 edges per node per table by default)."""
+    import torch
+    from minitchess_alphazero_amd import _lib
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    ref = _engine(16, 16, seed_base=3)
+    ref.set_weights(net)
+    st_ref = ref.play()
+    r_ref = ref.records()
+    assert st_ref['pool_edges'] == 0
+    small = _engine(16, 16, seed_base=3)
+    small.set_weights(net)
+    small.set_edge_capacity(64, 1 << 21)
+    st = small.play()
+    r = small.records()
+    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+        assert np.array_equal(r[key], r_ref[key]), key
+    assert st['pool_edges'] > 0 and st['max_edges'] <= 64
+    small.set_edge_capacity(64, 256)
+    with pytest.raises(_lib.MtazError, match='edge-capacity'):
+        small.play()
 
 
 def test_numpy1_cast_mode_vs_oracle():
@@ -81,21 +146,6 @@ def test_host_torch_net_matches_reference_trace():
     eng = _engine(1, gm['sims'])
     recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=TorchNetEvaluator(seed0_network()))
     assert compare_records(recs[0], gm['moves'])[2] is None
-
-
-def test_gpu_net_move_identity_vs_reference_trace(record_property):
-    """L3: the whole search on the GPU (network included) vs the reference trace."""
-    import torch
-    from minitchess_alphazero_amd.network import Network
-    gm = load_golden('trees')['net_seed0'][0]
-    eng = _engine(1, gm['sims'])
-    torch.manual_seed(0)
-    eng.set_weights(Network())
-    recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=None)
-    same, total, first = compare_records(recs[0], gm['moves'])
-    record_property('move_identity', f'{same}/{total}')
-    print(f'GPU-net move identity vs reference: {same}/{total} (first divergence: {first})')
-    assert first is None or first >= 10
 
 
 def test_cpp_driver_equals_python_driver():

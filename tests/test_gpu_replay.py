@@ -176,3 +176,24 @@ def test_learn_puppet_uses_ring():
     assert lp._replay is not None and len(lp._replay) == len(rec)
     out = lp.update(encode=False)
     assert np.isfinite(out['loss']) and len(lp._replay) == 0
+
+
+def test_both_push_paths_share_the_ring_in_arrival_order():
+    """A GPU LearnPuppet puts push_data rows (dict rows, the MQTT path) and push_records rows
+    (packed engine rows) into one HBM ring in push order: the ring equals the reference collate of
+    the rows in that order (exp/dataset.py:12-13 keeps one dataset), with no host copy kept."""
+    from minitchess_alphazero_amd.learner import LearnPuppet, ResidentBatches
+    rec = _engine_records(6, 8, seed=4)
+    rows = rec.to_rows()
+    n = len(rows)
+    a, b = n // 3, 2 * n // 3
+    lp = LearnPuppet('learner', 32, 1, {'lr': 0.02}, device='cuda', max_length=n - 5)
+    lp.push_data(rows[:a])
+    lp.push_records(rec.slice(a, b), 1)
+    lp.push_data(rows[b:])
+    assert lp._arrivals == [] and len(lp._replay) == n - 5       # deque(maxlen): the 5 oldest fell out
+    ref = ResidentBatches(rows[5:], 'cuda')
+    got = _rows_of(lp._replay, n - 5)
+    want = [t.cpu() for t in ref.gather(torch.arange(n - 5, device='cuda'))]
+    for g, w in zip(got, want):
+        assert torch.equal(g, w)

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Train the round-3 STRESS checkpoint: a network trained by the reference learner's update
+(exp/learner.py:72-94, minitchess_alphazero_amd.learner) in the C5 self-play loop on one GPU, to
+the regime the deployed learner drives toward: peaked priors (legal-logit spread >= 10) and
+trunk activations in the thousands.  The weights are data: the checkpoint is committed under
+tests/golden/stress/ with its sha256 and the reference network's outputs on it
+(tests/golden/make_golden_r3.py).
+
+For each learning rate in --lrs the loop starts from torch.manual_seed(0); Network() and runs
+--iterations updates (self-play of --games games at --sims sims, then one learner update of
+batch 32, 1 epoch).  After every update the network is measured in eval mode (the mode the
+self-play kernels fold) on up to 2,048 positions of that iteration's self-play:
+  trunk_max     max |activation| over every trunk conv block's output and the residual stream
+  spread_max    max over positions of (max - min) of the legal logits
+  spread_med    median of the same
+  pmax_med      median of the largest legal prior
+  value_std     std of the value over the positions (a collapsed value head has ~0)
+The first learning rate whose final network has trunk_max >= --min-trunk, spread_max >= 10 and
+value_std >= 0.05 is saved (--save, safetensors); --save-lr forces one.
+Output: one JSON line per iteration on stdout, a summary line at the end.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def measure(net, rec, device, max_pos=2048):
+    import copy
+    from minitchess_alphazero_amd.learner import encode_positions
+    net = copy.deepcopy(net).to(device)
+    n = min(len(rec), max_pos)
+    idx = np.linspace(0, len(rec) - 1, n).astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(rec.k)[:-1]])
+    tok, clk = encode_positions(rec.pos[idx], device)
+    acts = []
+    hooks = [m.register_forward_hook(lambda _m, _i, o: acts.append(float(o.detach().abs().max())))
+             for m in net.resbody.modules() if type(m).__name__ in ('_ConvBN', '_Residual')]
+    net.eval()
+    with torch.no_grad():
+        logits, value = net((tok, clk))
+    for h in hooks:
+        h.remove()
+    logits = logits.double().cpu().numpy()
+    value = value.double().cpu().numpy().reshape(-1)
+    spreads, pmax = [], []
+    for j, i in enumerate(idx):
+        codes = rec.codes[starts[i]:starts[i] + rec.k[i]].astype(np.int64)
+        lg = logits[j, codes]
+        spreads.append(lg.max() - lg.min())
+        e = np.exp(lg - lg.max())
+        pmax.append(float((e / e.sum()).max()))
+    return {'trunk_max': max(acts), 'spread_max': float(np.max(spreads)), 'spread_med': float(np.median(spreads)),
+            'pmax_med': float(np.median(pmax)), 'value_std': float(value.std()), 'value_min': float(value.min()),
+            'value_max': float(value.max()), 'logit_absmax': float(np.abs(logits).max()), 'positions': int(n)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--lrs', default='0.003,0.01,0.03')
+    ap.add_argument('--iterations', type=int, default=24)
+    ap.add_argument('--games', type=int, default=512)
+    ap.add_argument('--sims', type=int, default=32)
+    ap.add_argument('--min-trunk', type=float, default=1000.0)
+    ap.add_argument('--save', default='')
+    ap.add_argument('--save-lr', type=float, default=None)
+    args = ap.parse_args()
+    from minitchess_alphazero_amd.build import build
+    build(verbose=False)
+    from minitchess_alphazero_amd.loop import run_loop
+    dev = torch.device('cuda', 0)
+    torch.use_deterministic_algorithms(False)
+    summary, finals = [], {}
+    for lr in [float(x) for x in args.lrs.split(',')]:
+        t0 = time.time()
+        last = {}
+
+        def on_it(it, net, rec, h):
+            m = measure(net, rec, dev)
+            m.update({'lr': lr, 'iteration': it, 'loss': h['loss'], 'plies_per_game': h['plies_per_game'],
+                      'elapsed_s': round(time.time() - t0, 1)})
+            last.clear()
+            last.update(m)
+            print(json.dumps(m), flush=True)
+
+        _hist, net = run_loop(args.iterations, args.games, args.sims, lr=lr, device=0, log=lambda s: None,
+                              on_iteration=on_it)
+        finals[lr] = {k: v.detach().cpu().clone().contiguous() for k, v in net.state_dict().items()}
+        ok = (last['trunk_max'] >= args.min_trunk and last['spread_max'] >= 10 and last['value_std'] >= 0.05)
+        summary.append(dict(last, meets=ok))
+    pick = args.save_lr
+    if pick is None:
+        for s in summary:
+            if s['meets']:
+                pick = s['lr']
+                break
+    out = {'summary': summary, 'picked_lr': pick, 'iterations': args.iterations, 'games': args.games,
+           'sims': args.sims}
+    if pick is not None and args.save:
+        from safetensors.torch import save_file
+        os.makedirs(os.path.dirname(os.path.abspath(args.save)), exist_ok=True)
+        save_file(finals[pick], args.save)
+        out['saved'] = args.save
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()
