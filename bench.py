@@ -164,7 +164,8 @@ def main():
     ap.add_argument('--default-sims', type=int, default=36,
                     help="one more timed step at the repo's default sims per move (app/base.py:25: 36; 0 = skip), "
                          'reported with its CPU baseline as at_repo_default_sims')
-    ap.add_argument('--no-memo', action='store_true', help='evaluate every leaf (Engine.set_memo(False))')
+    ap.add_argument('--memo', type=int, default=1, choices=[0, 1, 2],
+                    help='leaf memo: 1 = per game (default), 2 = per game + batch, 0 = evaluate every leaf')
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
     ap.add_argument('--weights', default='', help='state_dict file (safetensors or torch.save) instead of random '
                                                   'init (BASELINE config 3: tests/golden/c3/c3.safetensors)')
@@ -186,6 +187,10 @@ def main():
     import torch
     rank = int(os.environ.get('RANK', 0))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    # this rank's disjoint slice of the host cores and its host-thread budget (launch.rank_host_share)
+    from minitchess_alphazero_amd.launch import pin_rank
+    host_threads = pin_rank(local, int(os.environ.get('LOCAL_WORLD_SIZE', world)))
+    torch.set_num_threads(host_threads)
     dist = None
     device = local if args.device is None else args.device
     red_device = torch.device('cuda', device)
@@ -230,7 +235,8 @@ def main():
         torch.manual_seed(0)                      # random-init weights of the reference architecture
         net_for_engine = Network()
     eng.set_weights(net_for_engine)
-    eng.set_memo(not args.no_memo)
+    eng.set_memo(args.memo)
+    eng.set_host_threads(min(16, host_threads))
     eng.set_precision(args.precision)
     eng.set_net_variant(args.net_variant)
     eng.set_timing(True)
@@ -245,7 +251,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    KEYS = ('sims', 'nn_evals', 'memo_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
+    KEYS = ('sims', 'nn_evals', 'memo_hits', 'memo_batch_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
             'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms')
 
     def timed(engine, steps, label):
@@ -273,6 +279,7 @@ def main():
                 'nn_evals_per_game': tot['nn_evals'] / games, 'memo_hits_per_game': tot['memo_hits'] / games,
                 'nn_evals_reference_per_game': ref_evals / games,
                 'memo_hit_frac': tot['memo_hits'] / ref_evals if ref_evals else 0.0,
+                'memo_batch_hit_frac': tot['memo_batch_hits'] / ref_evals if ref_evals else 0.0,
                 'nn_evals_per_s': tot['nn_evals'] / dt, 'nn_evals_reference_per_s': ref_evals / dt,
                 'terminal_sims_per_game': tot['terminal_sims'] / games, 'decisive_games': int(tot['decisive']),
                 'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12}
@@ -302,7 +309,8 @@ def main():
         eng36.set_net_variant(args.net_variant)
         eng36.set_timing(True)
         eng36.set_pipeline(args.groups)
-        eng36.set_memo(not args.no_memo)
+        eng36.set_memo(args.memo)
+        eng36.set_host_threads(min(16, host_threads))
         eng36.evaluate(np.stack([start_position()] * 8))
         dt3, tot3, prec3 = timed(eng36, 1, f'{args.default_sims} sims')
         at_default = {'sims_per_move': args.default_sims, 'value': G * world / dt3, 'unit': 'games/s', 'steps': 1,

@@ -159,13 +159,15 @@ int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_agent1);
  * while another's network occupies the GPU.  Games keep their global seeds, so results are
  * identical for any group count.  Applies to full-batch mtaz_play(h, n_games, 0) only. */
 int mtaz_set_pipeline(mtaz_engine* h, int groups);
-/* Leaf memo (1 = per game, the default; 0 = off).  The reference evaluates its network on every
- * leaf it expands (exp/agent.py:64-71), a pure function of the position; each of a game's two
- * agents keeps its own table (app/base.py:113), so a position one agent expanded earlier is
- * evaluated again when the other agent reaches it.  With the memo the second expansion copies the
- * first one's legal list, priors and value (or terminal value) from the other table: every table,
- * visit count and move is unchanged, the network runs on fewer leaves.  Off automatically when
- * the agents use different weight slots (mtaz_set_agent_slots). */
+/* Leaf memo (1 = per game, the default; 2 = per game + batch; 0 = off).  The reference evaluates
+ * its network on every leaf it expands (exp/agent.py:64-71), a pure function of the position; each
+ * of a game's two agents keeps its own table (app/base.py:113), so a position one agent expanded
+ * earlier is evaluated again when the other agent reaches it.  With the memo the second expansion
+ * copies the first one's legal list, priors and value (or terminal value) from the other table:
+ * every table, visit count and move is unchanged, the network runs on fewer leaves.  Mode 2 also
+ * keeps every evaluated position of the play (all games, until the next mtaz_play, mtaz_clear_trees
+ * of all tables or mtaz_set_weights) in an HBM table that later simulations of any game read.  Off
+ * automatically when the agents use different weight slots (mtaz_set_agent_slots). */
 int mtaz_set_memo(mtaz_engine* h, int mode);
 /* Edge storage of the MCTS tables (exp/agent.py:29-36 keeps a list of Q/N/P per node; here a
  * node's children are a contiguous edge range).  Each of the 2 * n_games tables owns a region of

@@ -97,7 +97,24 @@ struct Leaves {
   Pos* pos;               // [G]
   float* P;               // [G*KMAX] priors (softmax over the legal logits)
   float* v;               // [G]
-  uint8_t* ghit;          // [G] 1 when game g's simulation took its leaf from the memo
+  uint8_t* ghit;          // [G] 1 / 2 when game g's simulation took its leaf from the game / batch memo
+};
+
+// Batch leaf memo (Params::memo == 2): network results of the positions this engine evaluated
+// since the play started, shared by all its games.  Open addressing on the packed position
+// (linear probing); k_backup inserts each evaluated leaf (a slot claimed by atomicCAS on its
+// state: 0 empty, 1 being written, 2 ready), k_select of later simulations looks positions up.
+// Positions with more than MEMO_K legal moves are not kept.
+constexpr int MEMO_K = 32;
+constexpr uint32_t MEMO_PROBES = 64;   // insert and lookup give up after this many slots (a full table only loses hits)
+struct BatchMemo {
+  uint32_t* state;        // [cap]
+  Pos* key;               // [cap]
+  float* v;               // [cap]
+  uint16_t* k;            // [cap]
+  uint16_t* codes;        // [cap][MEMO_K]
+  float* P;               // [cap][MEMO_K]
+  uint32_t cap;           // power of two (0 = not allocated)
 };
 
 struct Params {
@@ -110,11 +127,12 @@ struct Params {
   const double* sqrt_tab; // sqrt(n) for n < sqrt_n (exactly what np.sqrt returns)
   int sqrt_n;
   int32_t* err;
-  // leaf memo (0 = off, 1 = per game): a position the game's other agent already expanded takes
-  // its legal list, priors and value from that agent's table instead of a network evaluation.
-  // The network is a pure function of the position (exp/agent.py:64-71 evaluates
-  // process_observation(fen) alone), so the tables, and every result, are those without the memo.
-  // Off when the two agents search with different networks (arena).
+  // leaf memo (0 = off, 1 = per game, 2 = per game + batch): a position the game's other agent
+  // already expanded takes its legal list, priors and value from that agent's table (and with 2, a
+  // position any game of the batch had evaluated, from the BatchMemo) instead of a network
+  // evaluation.  The network is a pure function of the position (exp/agent.py:64-71 evaluates
+  // process_observation(fen) alone) and per-board deterministic, so the tables, and every result,
+  // are those without the memo.  Off when the two agents search with different networks (arena).
   int memo;
 };
 
@@ -123,6 +141,7 @@ struct Dev {
   Games gm;
   Leaves lf;
   Params pr;
+  BatchMemo bm;
 };
 
 // ---- network -------------------------------------------------------------------------
@@ -233,6 +252,7 @@ void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32
 void launch_net_z_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
                           float* values_out, unsigned long long* stamps, hipStream_t s, int variant);
 void launch_backup(const Dev& d, hipStream_t s);
+void launch_memo_clear(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);
 void launch_gather_leaf_codes(const Dev& d, uint16_t* codes_out, int32_t* k_out, hipStream_t s);

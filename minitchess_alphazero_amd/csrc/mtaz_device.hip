@@ -432,12 +432,37 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
         // expansion would compute (rules and network are functions of the position alone), and
         // the simulation backs up here instead of queueing a leaf.  Tree t ^ 1 is idle during
         // tree t's search (the agents alternate by ply), so it is read without synchronisation.
+        // With the batch memo (Params::memo 2), a position another game evaluated in an earlier
+        // simulation of this play comes from the BatchMemo the same way.
         uint32_t m = NONE;
         NodeHdr mh{0u, 0u, 0u, 0.0f};
+        const uint16_t* msrc_code = nullptr;
+        const float* msrc_P = nullptr;
+        uint8_t mkind = 0;   // 1 = the game's other table, 2 = the batch memo
         if (D.pr.memo) {
           uint32_t s2;
           m = tree_find(T, t ^ 1, pos, &s2);
-          if (m != NONE) mh = T.node_hdr[(size_t)(t ^ 1) * T.NC + m];
+          if (m != NONE) {
+            mkind = 1;
+            mh = T.node_hdr[(size_t)(t ^ 1) * T.NC + m];
+            msrc_code = T.e_code + mh.e0;
+            msrc_P = T.e_P + mh.e0;
+          } else if (D.pr.memo >= 2) {
+            const BatchMemo& B = D.bm;
+            const uint32_t mask = B.cap - 1;
+            uint32_t h = pos_hash(pos) & mask;
+            for (uint32_t probe = 0; probe < MEMO_PROBES; ++probe, h = (h + 1) & mask) {
+              if (B.state[h] == 0u) break;
+              if (pos_eq(B.key[h], pos)) {
+                m = h;
+                mkind = 2;
+                mh = NodeHdr{0u, 0u, (uint32_t)B.k[h], B.v[h]};
+                msrc_code = B.codes + (size_t)h * MEMO_K;
+                msrc_P = B.P + (size_t)h * MEMO_K;
+                break;
+              }
+            }
+          }
         }
         int k;
         bool term;
@@ -486,7 +511,7 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
                 D.lf.gpos[g] = pos;
                 D.gm.path_len[g] = depth;
               } else {
-                D.lf.ghit[g] = 1;
+                D.lf.ghit[g] = mkind;
               }
             }
             if (pedge != NONE) T.e_child[pedge] = nn;
@@ -497,11 +522,10 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
         ne0 = __shfl(ne0, 0, 64);
         if (nn != NONE) {
           if (!term) {
-            const size_t msrc = mh.e0;
             for (int c = lane; c < k; c += 64) {
               const size_t e = (size_t)ne0 + c;
-              T.e_code[e] = m != NONE ? T.e_code[msrc + c] : s_l.sorted[c];
-              T.e_P[e] = m != NONE ? T.e_P[msrc + c] : 0.f;
+              T.e_code[e] = m != NONE ? msrc_code[c] : s_l.sorted[c];
+              T.e_P[e] = m != NONE ? msrc_P[c] : 0.f;
               T.e_Q[e] = 0.0;
               T.e_N[e] = 0;
               T.e_child[e] = NONE;
@@ -598,14 +622,14 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
 // The leaf batch in game order: one workgroup; per chunk of 4,096 games thread i holds games
 // 4i..4i+3 in registers (their leaf, agent and position in one round of loads: loads placed after
 // the stores would wait for them), a block scan of the per-thread counts places its leaves.
-// Also logs the count and the number of memo hits (count_log[0..1], when given).
+// Also logs the count and the memo hits of the game and batch memos (count_log[0..2], when given).
 __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restrict__ count_log) {
   constexpr int PER = 4;
   __shared__ int s_w[16];
-  __shared__ int s_hits;
+  __shared__ int s_hits[2];
   const int G = D.pr.G, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) s_hits = 0;
-  int base = 0, hits = 0;
+  if (tid < 2) s_hits[tid] = 0;
+  int base = 0, hits = 0, bhits = 0;
   for (int c0 = 0; c0 < G; c0 += 1024 * PER) {
     const int g0 = c0 + tid * PER;
     uint32_t nd[PER];
@@ -618,7 +642,9 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
       nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
       ag[j] = in ? D.gm.agent[g0 + j] : 0;
       ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
-      hits += in ? (int)D.lf.ghit[g0 + j] : 0;
+      const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
+      hits += hk == 1;
+      bhits += hk == 2;
     }
 #pragma unroll
     for (int j = 0; j < PER; ++j) c += nd[j] != NONE;
@@ -646,14 +672,19 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     }
     base += tot;
   }
-  for (int o = 32; o > 0; o >>= 1) hits += __shfl_xor(hits, o, 64);
-  if (lane == 0 && hits) atomicAdd(&s_hits, hits);
+  for (int o = 32; o > 0; o >>= 1) {
+    hits += __shfl_xor(hits, o, 64);
+    bhits += __shfl_xor(bhits, o, 64);
+  }
+  if (lane == 0 && hits) atomicAdd(&s_hits[0], hits);
+  if (lane == 0 && bhits) atomicAdd(&s_hits[1], bhits);
   __syncthreads();
   if (tid == 0) {
     *D.lf.count = base;
     if (count_log) {
       count_log[0] = base;
-      count_log[1] = s_hits;
+      count_log[1] = s_hits[0];
+      count_log[2] = s_hits[1];
     }
   }
 }
@@ -695,9 +726,46 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
   const int k = hdr_k(hd);
   for (int c = lane; c < k; c += 64) T.e_P[(size_t)hd.e0 + c] = D.lf.P[(size_t)i * KMAX + c];
   if (lane == 0) T.node_hdr[nbase + n].tval = D.lf.v[i];   // kept for the leaf memo (Params::memo)
+  if (D.pr.memo >= 2 && D.bm.cap && k <= MEMO_K) {
+    // batch memo insert: claim a slot (0 -> 1), write, publish (-> 2); a slot another leaf of this
+    // launch claimed is passed over (at worst a position is kept twice, with identical results)
+    const BatchMemo& B = D.bm;
+    const Pos p = D.lf.pos[i];
+    uint32_t slot = NONE;
+    if (lane == 0) {
+      const uint32_t mask = B.cap - 1;
+      uint32_t h = pos_hash(p) & mask;
+      for (uint32_t probe = 0; probe < MEMO_PROBES; ++probe, h = (h + 1) & mask) {
+        const uint32_t st = atomicCAS(&B.state[h], 0u, 1u);
+        if (st == 0u) {
+          slot = h;
+          break;
+        }
+        if (st == 2u && pos_eq(B.key[h], p)) break;
+      }
+    }
+    slot = __shfl(slot, 0, 64);
+    if (slot != NONE) {
+      for (int c = lane; c < k; c += 64) {
+        B.codes[(size_t)slot * MEMO_K + c] = T.e_code[(size_t)hd.e0 + c];
+        B.P[(size_t)slot * MEMO_K + c] = D.lf.P[(size_t)i * KMAX + c];
+      }
+      if (lane == 0) {
+        B.key[slot] = p;
+        B.v[slot] = D.lf.v[i];
+        B.k[slot] = (uint16_t)k;
+        __threadfence();
+        atomicExch(&B.state[slot], 2u);
+      }
+    }
+  }
   const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
   backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i], lane);
+}
+
+void launch_memo_clear(const Dev& d, hipStream_t s) {
+  if (d.bm.cap) (void)hipMemsetAsync(d.bm.state, 0, (size_t)d.bm.cap * 4, s);
 }
 
 void launch_backup(const Dev& d, hipStream_t s) {

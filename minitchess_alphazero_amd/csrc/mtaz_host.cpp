@@ -450,7 +450,7 @@ struct PlyRec {
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
-  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_COUNT
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_COUNT
 };
 
 // Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
@@ -597,6 +597,7 @@ struct mtaz_engine {
   float* wyrange = nullptr;
   std::vector<void*> allocs;
   std::vector<void*> edge_allocs;       // the edge arrays (alloc_edges; mtaz_set_edge_capacity replaces them)
+  std::vector<void*> memo_allocs;       // the batch memo (ensure_batch_memo)
   float* wbuf = nullptr;
   // scratch
   int32_t* d_actions = nullptr;
@@ -647,6 +648,7 @@ struct mtaz_engine {
     for (auto e : ev) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : edge_allocs) (void)hipFree(p);
+    for (void* p : memo_allocs) (void)hipFree(p);
     if (d.gm.noise) (void)hipFree(d.gm.noise);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -779,8 +781,8 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&h->d_leaf_codes, (size_t)G * KMAX));
   ECHK(h->dalloc(&h->d_leaf_k, G));
   ECHK(h->dalloc(&h->d_trees, T));
-  h->count_log_cap = h->sims * (2 * max_moves + 8);   // waves; two ints each (leaves, memo hits)
-  ECHK(h->dalloc(&h->d_count_log, 2 * (size_t)h->count_log_cap));
+  h->count_log_cap = h->sims * (2 * max_moves + 8);   // waves; three ints each (leaves, game / batch memo hits)
+  ECHK(h->dalloc(&h->d_count_log, 3 * (size_t)h->count_log_cap));
   // exact sqrt(N.sum()) table: N.sum() <= sims * searches per agent
   const int sqn = tr.NC + 2;
   std::vector<double> sq(sqn);
@@ -866,6 +868,8 @@ static int check_err(mtaz_engine* h) {
 }
 
 // ---- weights --------------------------------------------------------------------------
+static int clear_batch_memo(mtaz_engine* h);
+
 extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, const int64_t* numels, int n) {
   if (n != 133) return set_err(MTAZ_E_FAIL, "expected 133 state_dict tensors (num_batches_tracked skipped), got %d", n);
   HIPCHK(hipSetDevice(h->device));
@@ -1193,6 +1197,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.convz = h->wxbuf + o_wz;
   h->w.stemz = h->wxbuf + o_sz;
   h->weights_ok = true;
+  ECHK(clear_batch_memo(h));   // results of the previous network
   return 0;
 }
 
@@ -1308,9 +1313,44 @@ extern "C" int mtaz_set_weights_slot(mtaz_engine* h, int slot, const float* cons
   return rc;
 }
 
-// the memo shares leaf results between a game's two tables: only when both agents search with the
-// same network
+// the memo shares leaf results between a game's two tables (and the batch's games): only when both
+// agents search with the same network
 static void sync_memo(mtaz_engine* h) { h->d.pr.memo = h->agent_slot[0] == h->agent_slot[1] ? h->memo : 0; }
+
+// The batch memo's table: 2 slots per possible evaluation of a play (2 G tables x move_cap searches x
+// sims), a power of two, at most 2^28 slots (222 B each).
+static int ensure_batch_memo(mtaz_engine* h) {
+  if (h->memo < 2 || h->d.bm.cap) return 0;
+  const int max_moves = h->move_cap > 0 ? h->move_cap : 200;
+  const uint64_t want = 2ull * 2 * (uint64_t)h->G * (uint64_t)max_moves * (uint64_t)h->sims;
+  uint64_t cap = 1024;
+  while (cap < want && cap < (1ull << 28)) cap <<= 1;
+  BatchMemo& B = h->d.bm;
+  auto grab = [&](auto** p, size_t elt) -> int {
+    void* q = nullptr;
+    HIPCHK(hipMalloc(&q, cap * elt));
+    h->memo_allocs.push_back(q);
+    *p = (std::remove_reference_t<decltype(*p)>)q;
+    return 0;
+  };
+  ECHK(grab(&B.state, 4));
+  ECHK(grab(&B.key, sizeof(Pos)));
+  ECHK(grab(&B.v, 4));
+  ECHK(grab(&B.k, 2));
+  ECHK(grab(&B.codes, 2 * MEMO_K));
+  ECHK(grab(&B.P, 4 * MEMO_K));
+  B.cap = (uint32_t)cap;
+  HIPCHK(hipMemset(B.state, 0, cap * 4));
+  return 0;
+}
+
+// empties the batch memo (new weights, new play)
+static int clear_batch_memo(mtaz_engine* h) {
+  if (!h->d.bm.cap) return 0;
+  launch_memo_clear(h->d, h->stream);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
 
 extern "C" int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_agent1) {
   if ((slot_agent0 | slot_agent1) & ~1) return set_err(MTAZ_E_FAIL, "weight slots must be 0 or 1");
@@ -1321,8 +1361,11 @@ extern "C" int mtaz_set_agent_slots(mtaz_engine* h, int slot_agent0, int slot_ag
 }
 
 extern "C" int mtaz_set_memo(mtaz_engine* h, int mode) {
-  if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "memo mode must be 0 (off) or 1 (per game)");
+  if (mode < 0 || mode > 2) return set_err(MTAZ_E_FAIL, "memo mode must be 0 (off), 1 (per game) or 2 (per game + batch)");
+  HIPCHK(hipSetDevice(h->device));
   h->memo = mode;
+  ECHK(ensure_batch_memo(h));
+  ECHK(clear_batch_memo(h));
   sync_memo(h);
   return 0;
 }
@@ -1415,6 +1458,7 @@ extern "C" int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n) {
     if (trees[i] < 0 || trees[i] >= 2 * h->G) return set_err(MTAZ_E_FAIL, "tree index %d out of range", trees[i]);
   HIPCHK(hipMemcpyAsync(h->d_trees, trees, n * 4, hipMemcpyHostToDevice, h->stream));
   launch_reset_trees(h->d, h->d_trees, n, !all.empty(), h->stream);
+  if (!all.empty()) ECHK(clear_batch_memo(h));   // all tables cleared (a new play): a new batch
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
@@ -1469,7 +1513,7 @@ static int sim_gpu(mtaz_engine* h, int sim) {
     eb = h->ev[4 * h->wave + 2];
     ee = h->ev[4 * h->wave + 3];
   }
-  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + 2 * (size_t)h->wave : nullptr, em);
+  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + 3 * (size_t)h->wave : nullptr, em);
   launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, eb, ee);
   launch_backup(h->d, h->stream);
   HIPCHK(hipGetLastError());
@@ -1717,6 +1761,7 @@ static int play_groups(mtaz_engine* h) {
     p->timing = h->timing;
     p->host_threads = std::max(1, h->host_threads / ng);   // the groups share this engine's threads
     p->memo = h->memo;
+    ECHK(ensure_batch_memo(p));
     sync_memo(p);
     p->seed_base = h->seed_base + (uint64_t)i * Gp;
   }
@@ -1911,13 +1956,14 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   for (int g = 0; g < G; ++g) h->final_outcome[g] = outcome_v[g];
   // stats
   const int nlog = std::min(h->wave, h->count_log_cap);
-  std::vector<int32_t> clog(2 * (size_t)nlog), counts(nlog);
+  std::vector<int32_t> clog(3 * (size_t)nlog), counts(nlog);
   if (nlog) HIPCHK(hipMemcpy(clog.data(), h->d_count_log, clog.size() * 4, hipMemcpyDeviceToHost));
-  double evals = 0, hits = 0;
+  double evals = 0, hits = 0, bhits = 0;
   for (int wv = 0; wv < nlog; ++wv) {
-    counts[wv] = clog[2 * wv];
-    evals += clog[2 * wv];
-    hits += clog[2 * wv + 1];
+    counts[wv] = clog[3 * wv];
+    evals += clog[3 * wv];
+    hits += clog[3 * wv + 1];
+    bhits += clog[3 * wv + 2];
   }
   double trunk_ms = 0, trunk_boards = 0, select_ms = 0, compact_ms = 0;
   if (h->timing) {
@@ -1947,8 +1993,9 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   }
   h->stats[ST_PLIES] = (double)plies;
   h->stats[ST_NN_EVALS] = evals;                              // network evaluations computed
-  h->stats[ST_MEMO_HITS] = hits;                              // leaves the memo supplied
-  h->stats[ST_TERMINAL_SIMS] = h->stats[ST_SIMS] - evals - hits;
+  h->stats[ST_MEMO_HITS] = hits + bhits;                      // leaves the memo supplied
+  h->stats[ST_MEMO_BATCH_HITS] = bhits;                       //   of which from the batch memo
+  h->stats[ST_TERMINAL_SIMS] = h->stats[ST_SIMS] - evals - hits - bhits;
   h->stats[ST_TRUNK_MS] = trunk_ms;
   h->stats[ST_TRUNK_BOARDS] = trunk_boards;
   h->stats[ST_WAVES] = h->wave;

@@ -24,7 +24,8 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
-              'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap']
+              'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap',
+              'memo_batch_hits']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
@@ -112,12 +113,14 @@ class Engine:
         Results are identical for any group count (games keep their global seeds)."""
         _lib.check(self.L.mtaz_set_pipeline(self.h, int(groups)))
 
-    def set_memo(self, on=True):
-        """Leaf memo (default on): a position the game's other agent already expanded takes its
-        legal list, priors and value from that agent's table instead of the network (results
-        unchanged; include/mtaz.h mtaz_set_memo).  stats()['nn_evals'] counts the evaluations
-        computed, 'memo_hits' the ones the memo supplied; their sum is the reference's count."""
-        _lib.check(self.L.mtaz_set_memo(self.h, 1 if on else 0))
+    def set_memo(self, mode=1):
+        """Leaf memo: 1 (default, or True) = a position the game's other agent already expanded
+        takes its legal list, priors and value from that agent's table instead of the network;
+        2 = also positions any game of the batch evaluated earlier in the play; 0 (False) = off.
+        Results unchanged (include/mtaz.h mtaz_set_memo).  stats()['nn_evals'] counts the
+        evaluations computed, 'memo_hits' the ones the memo supplied ('memo_batch_hits' of them from
+        the batch memo); evaluations + hits is the reference's count."""
+        _lib.check(self.L.mtaz_set_memo(self.h, int(mode)))
 
     def set_edge_capacity(self, per_tree, pool):
         """Edge storage: `per_tree` edges in each table's own region plus a pool of `pool` edges

@@ -59,6 +59,40 @@ def spawn_ranks(n, argv, env=None, poll_s=0.2):
     return rc
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (None: unlimited or unknown)."""
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        return None if q == 'max' else float(q) / float(period)
+    except (OSError, ValueError):
+        return None
+
+
+def rank_host_share(local_rank, local_world, cores=None, quota=None):
+    """This rank's slice of the host: the ranks on a node split the process's affinity mask into
+    disjoint contiguous core ranges, and its usable CPUs (the smaller of the mask and the cgroup
+    quota) into equal thread budgets, so N ranks of host work (Dirichlet draws, action choice,
+    torch) do not oversubscribe the cores the node grants.  -> (cores, threads); cores is None
+    when the mask has fewer cores than ranks (no pinning then)."""
+    if cores is None:
+        cores = sorted(os.sched_getaffinity(0))
+    if quota is None:
+        quota = cgroup_cpu_quota()
+    usable = len(cores) if quota is None else max(1, min(len(cores), int(quota)))
+    threads = max(1, usable // max(1, local_world))
+    per = len(cores) // max(1, local_world)
+    mine = cores[local_rank * per:(local_rank + 1) * per] if per >= 1 else None
+    return mine, threads
+
+
+def pin_rank(local_rank, local_world):
+    """Apply rank_host_share to this process (before it starts threads); returns the thread budget."""
+    mine, threads = rank_host_share(local_rank, local_world)
+    if mine and local_world > 1:
+        os.sched_setaffinity(0, mine)
+    return threads
+
+
 def main_or_spawn(n_requested, script):
     """For a script started as `python script ... --gpus N`: returns the world size this process
     belongs to, after checking it against N, or (with no launcher and N > 1) runs N ranks of the

@@ -173,6 +173,8 @@ def main(argv=None):
     args = ap.parse_args(argv)
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    from .launch import pin_rank
+    torch.set_num_threads(pin_rank(local, int(os.environ.get('LOCAL_WORLD_SIZE', world))))
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -135,22 +135,38 @@ class RecordedEvaluator:
         return np.asarray(P, np.float32), v
 
 
-def explain_divergence(gpu_leaves, ref_evaluator, sims, seed, gpu_moves, prior_tol=1e-5, value_tol=1e-5):
+class _LoggingEvaluator:
+    """Wraps an oracle evaluator; logs (fen, P, v, number of PUCT selections so far)."""
+
+    def __init__(self, inner, trace):
+        self.inner, self.trace, self.log = inner, trace, []
+
+    def evaluate(self, fen, legal_moves):
+        P, v = self.inner.evaluate(fen, legal_moves)
+        self.log.append((fen, np.asarray(P, np.float64), float(v), len(self.trace)))
+        return P, v
+
+
+def explain_divergence(gpu_leaves, ref_evaluator, sims, seed, gpu_moves, bound_scale=1.0):
     """Why a GPU-network game left the reference game.  Two oracle replays of game `seed`, one with
     the GPU's recorded leaf results (it must reproduce the GPU game exactly) and one with the
     reference network, record every PUCT selection; the first selection where they differ is the
-    flip.  Returns the reference's decision margin there (u of its choice - u of the GPU's choice),
-    the GPU run's opposite margin, and the largest margin the north_star tolerance allows:
-    priors within prior_tol and values within value_tol move u = Q + cpuct*P'*sqrt(S)/(1+N) of a
-    child by at most value_tol + prior_tol*sqrt(S) (Q is an average of backed-up values; the root
-    noise mix scales P by 0.75), so a flip between two children is explained by the tolerance when
-    margin_ref + margin_gpu <= 2*(value_tol + prior_tol*sqrt(S))."""
+    flip.  Until then both replays expanded the same leaves in the same order with the same
+    Dirichlet draws, so the only differences are the leaf results themselves: dP = the largest
+    |P_gpu - P_ref| and dv = the largest |v_gpu - v_ref| over the leaves evaluated before the flip,
+    MEASURED on this game.  They move u = Q + cpuct*P'*sqrt(S)/(1+N) of a child by at most
+    dv + dP*sqrt(S) (Q averages backed-up leaf values; the root mix scales P by 0.75), so the flip
+    is explained when the reference margin (u of its choice - u of the GPU's choice) plus the GPU
+    run's opposite margin is at most 2*(dv + dP*sqrt(S)) (+1e-12 for the rounding of u itself).
+    Returns both margins, dP, dv, the bound, and the bound the 1e-5 north_star tolerance would give.
+    bound_scale < 1 shrinks the measured bound (tests/test_explain_cpu.py: the bound is not loose)."""
     from oracle import selfplay
     tr_gpu, tr_ref = [], []
     rec_gpu = selfplay.play_games(RecordedEvaluator(gpu_leaves), 1, sims, seed_base=seed, trace=tr_gpu)[0]
     same, _total, first = compare_records(rec_gpu, gpu_moves)
     assert first is None, f'the oracle replay of the GPU leaves left the GPU game at ply {first}'
-    selfplay.play_games(ref_evaluator, 1, sims, seed_base=seed, trace=tr_ref)
+    ref_log = _LoggingEvaluator(ref_evaluator, tr_ref)
+    selfplay.play_games(ref_log, 1, sims, seed_base=seed, trace=tr_ref)
     for i, (a, b) in enumerate(zip(tr_ref, tr_gpu)):
         if a[0] != b[0] or a[2] != b[2]:
             assert a[0] == b[0], 'the replays reached different nodes without a differing selection'
@@ -158,8 +174,19 @@ def explain_divergence(gpu_leaves, ref_evaluator, sims, seed, gpu_moves, prior_t
             S = a[3]
             m_ref = float(u_ref[ar] - u_ref[ag])
             m_gpu = float(u_gpu[ag] - u_gpu[ar])
-            bound = 2 * (value_tol + prior_tol * np.sqrt(S))
+            dP = dv = 0.0
+            n_leaves = 0
+            for fen, P_ref, v_ref, t in ref_log.log:
+                if t > i:
+                    break
+                P_gpu, v_gpu = gpu_leaves[fen]
+                dP = max(dP, float(np.max(np.abs(np.asarray(P_gpu, np.float64) - P_ref))) if len(P_ref) else 0.0)
+                dv = max(dv, abs(float(v_gpu) - v_ref))
+                n_leaves += 1
+            bound = bound_scale * 2 * (dv + dP * np.sqrt(S)) + 1e-12
             return {'selection': i, 'node': a[0], 'ref_choice': ar, 'gpu_choice': ag, 'visits_at_node': S,
-                    'margin_ref': m_ref, 'margin_gpu': m_gpu, 'tolerance_bound': float(bound),
+                    'margin_ref': m_ref, 'margin_gpu': m_gpu, 'leaves_before_flip': n_leaves,
+                    'max_dP': dP, 'max_dv': dv, 'measured_bound': float(bound),
+                    'tolerance_bound_1e-5': float(2 * (1e-5 + 1e-5 * np.sqrt(S))),
                     'explained': bool(m_ref >= 0 and m_gpu >= 0 and m_ref + m_gpu <= bound)}
     return None

@@ -1,9 +1,10 @@
 """CPU: the L3 divergence explainer (helpers.explain_divergence) on a controlled perturbation.
 
 'GPU' leaf results = the synthetic evaluator's priors and values moved by up to 1e-4 x (priors
-relatively); the explainer runs with that deviation as its tolerance.  Where the perturbed game
-leaves the unperturbed one, it must find the first differing PUCT selection and report a near-tie
-inside the tolerance bound, and a 100x smaller tolerance must not explain it."""
+relatively).  Where the perturbed game leaves the unperturbed one, the explainer must find the
+first differing PUCT selection, measure the leaf deviations before it (no larger than the
+perturbation), and report a near-tie inside the bound they imply; the same bound shrunk 100x must
+not explain it."""
 import zlib
 
 import numpy as np
@@ -37,10 +38,11 @@ def test_explainer_finds_an_explained_near_tie():
         first = compare_records(gpu, ref)[2]
         if first is None:
             continue
-        flip = explain_divergence(table, base, 32, seed, gpu, prior_tol=1e-4, value_tol=1e-4)
+        flip = explain_divergence(table, base, 32, seed, gpu)
         assert flip is not None and flip['explained'], flip
-        assert 0 <= flip['margin_ref'] <= flip['tolerance_bound']
-        tight = explain_divergence(table, base, 32, seed, gpu, prior_tol=1e-6, value_tol=1e-6)
+        assert 0 <= flip['margin_ref'] <= flip['measured_bound']
+        assert 0 < flip['max_dv'] <= 1e-4 and 0 < flip['max_dP'] <= 1e-4 and flip['leaves_before_flip'] > 0
+        tight = explain_divergence(table, base, 32, seed, gpu, bound_scale=0.01)
         assert tight['selection'] == flip['selection'] and not tight['explained'], tight
         found = True
         break

@@ -36,13 +36,14 @@ def test_select_expand_backup_synthetic_vs_reference_traces():
             assert [r['reward'] for r in got] == [r['reward'] for r in gm['moves']]
 
 
-@pytest.mark.parametrize('memo,spill', [(True, False), (False, False), (True, True)],
-                         ids=['memo', 'no-memo', 'memo-pool-spill'])
+@pytest.mark.parametrize('memo,spill', [(1, False), (0, False), (1, True), (2, False)],
+                         ids=['memo', 'no-memo', 'memo-pool-spill', 'batch-memo'])
 def test_trees_bit_exact_vs_oracle(memo, spill):
     """Final transposition tables (Q, N, P, legal_moves, terminal, visited) equal the oracle's,
-    with the per-game leaf memo (the default) and without it, and with table regions of 40 edges
-    so that most nodes take their children from the shared edge pool.  The host evaluator sees
-    every leaf the engine asks for: all of the oracle's expansions without the memo, fewer with it."""
+    with the per-game leaf memo (the default), the per-game + batch memo and without a memo, and
+    with table regions of 40 edges so that most nodes take their children from the shared edge
+    pool.  The host evaluator sees every leaf the engine asks for: all of the oracle's expansions
+    without the memo, fewer with it."""
     from oracle.mcts import SyntheticEvaluator
     from oracle import selfplay
     ev = SyntheticEvaluator(salt=3)
@@ -77,26 +78,34 @@ def test_trees_bit_exact_vs_oracle(memo, spill):
 
 def test_leaf_memo_leaves_games_unchanged():
     """The leaf memo changes which leaves the network evaluates, not the games: with the GPU network,
-    memo on and off give identical records, and computed + memo-supplied evaluations equal the
-    evaluations without the memo (the reference's count: one per non-terminal expansion)."""
+    the per-game memo, the per-game + batch memo and no memo give identical records, and computed +
+    memo-supplied evaluations equal the evaluations without the memo (the reference's count: one
+    per non-terminal expansion).  The engine is played twice per mode: the batch memo starts empty
+    in every play."""
     import torch
     from minitchess_alphazero_amd.network import Network
     torch.manual_seed(0)
     net = Network()
     out = {}
-    for memo in (True, False):
+    for memo in (1, 2, 0):
         eng = _engine(32, 16, seed_base=11)
         eng.set_weights(net)
         eng.set_memo(memo)
+        first = eng.play()
         out[memo] = (eng.play(), eng.records())
-    (st_on, r_on), (st_off, r_off) = out[True], out[False]
-    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
-        assert np.array_equal(r_on[key], r_off[key]), key
-    assert st_off['memo_hits'] == 0 and st_on['memo_hits'] > 0
-    assert st_on['nn_evals'] + st_on['memo_hits'] == st_off['nn_evals']
-    assert st_on['terminal_sims'] == st_off['terminal_sims']
-    print(f"memo: {st_on['memo_hits']:.0f} of {st_off['nn_evals']:.0f} evaluations supplied "
-          f"({st_on['memo_hits'] / st_off['nn_evals']:.1%})")
+        assert first['nn_evals'] == out[memo][0]['nn_evals']
+    st_off, r_off = out[0]
+    assert st_off['memo_hits'] == 0
+    for memo in (1, 2):
+        st, r = out[memo]
+        for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+            assert np.array_equal(r[key], r_off[key]), (memo, key)
+        assert st['memo_hits'] > 0
+        assert st['nn_evals'] + st['memo_hits'] == st_off['nn_evals']
+        assert st['terminal_sims'] == st_off['terminal_sims']
+        print(f"memo {memo}: {st['memo_hits']:.0f} of {st_off['nn_evals']:.0f} evaluations supplied "
+              f"({st['memo_hits'] / st_off['nn_evals']:.1%}; batch memo {st['memo_batch_hits']:.0f})")
+    assert out[1][0]['memo_batch_hits'] == 0 and out[2][0]['memo_batch_hits'] > 0
 
 
 def test_edge_pool_spill_and_exhaustion():

@@ -5,11 +5,12 @@
     and v.item() of :69) vs the reference's softmax over its own logits, <= 1e-5 (north_star)
   * L3: self-play with the GPU network end to end vs the reference's games (every pi, action and
     reward), seed-0 net at 32 and 64 sims and the C3 net at 256.  Bit-exact move selection is the
-    target; a game may leave the reference game only at a near-tie that the permitted 1e-5
-    prior/value deviation can flip: the first PUCT selection where an oracle replay of the GPU's own
-    leaf results differs from the reference replay must have a reference margin below the bound
-    that tolerance implies (helpers.explain_divergence).  Identity rates and every divergence's
-    margin are written to gpurun_out/l3_identity.json
+    target; a game may leave the reference game only at a near-tie that the leaf deviations
+    MEASURED on that game can flip: at the first PUCT selection where an oracle replay of the GPU's
+    own leaf results differs from the reference replay, the two margins must sum to at most
+    2 (dv + dP sqrt(S)), dP and dv the largest prior and value deviations of the leaves evaluated
+    before it (helpers.explain_divergence).  Identity rates, every divergence's margins and its
+    measured dP, dv are written to gpurun_out/l3_identity.json
   * the terminal-revisit quirk (exp/agent.py:57-63 vs :75-77) through k_select
   * decisive games (reward back-fill, exp/callbacks.py:49-54; terminal handling) on the GPU
   * BASELINE config 3: the pinned trained checkpoint (tests/golden/make_golden_r2.py): network

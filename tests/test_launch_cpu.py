@@ -42,3 +42,21 @@ def test_bench_rejects_a_world_size_that_differs_from_gpus():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2
     assert '--gpus 2' in r.stderr
+
+
+def test_rank_host_share_splits_cores_and_threads():
+    """Ranks on a node get disjoint core ranges covering the mask, and thread budgets that together
+    stay within the usable CPUs (the smaller of the mask and the cgroup quota)."""
+    from minitchess_alphazero_amd.launch import rank_host_share
+    cores = list(range(16))
+    slices = [rank_host_share(r, 8, cores=cores, quota=None) for r in range(8)]
+    assert [s[1] for s in slices] == [2] * 8
+    got = [c for s in slices for c in s[0]]
+    assert got == cores
+    # a 192-CPU mask under a 16-CPU quota: 24 cores each, 2 threads each
+    big = [rank_host_share(r, 8, cores=list(range(192)), quota=16.0) for r in range(8)]
+    assert all(len(c) == 24 and t == 2 for c, t in big)
+    assert len({x for c, _ in big for x in c}) == 192
+    # more ranks than cores: no pinning, one thread each
+    assert rank_host_share(3, 8, cores=[0, 1, 2, 3], quota=None) == (None, 1)
+    assert rank_host_share(0, 1, cores=cores, quota=None) == (cores, 16)

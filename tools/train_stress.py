@@ -15,8 +15,13 @@ self-play kernels fold) on up to 2,048 positions of that iteration's self-play:
   spread_med    median of the same
   pmax_med      median of the largest legal prior
   value_std     std of the value over the positions (a collapsed value head has ~0)
-The first learning rate whose final network has trunk_max >= --min-trunk, spread_max >= 10 and
-value_std >= 0.05 is saved (--save, safetensors); --save-lr forces one.
+A network qualifies after update >= --min-iteration (the verdict asks for >= 20 updates) when
+trunk_max >= --min-trunk (activations in the thousands), spread_max >= --min-spread (peaked
+priors) and the largest |logit| <= --max-logit (beyond that, fp32's own rounding of the logits
+exceeds the 1e-5 prior budget, so no fp32 implementation could match another to it).  For each
+learning rate the loop stops at the first qualifying network; the first learning rate that
+produced one is saved (--save, safetensors).  GPU training is not bitwise reproducible, so the
+saved checkpoint is data: tests/golden/make_golden_r3.py pins it by sha256.
 Output: one JSON line per iteration on stdout, a summary line at the end.
 """
 import argparse
@@ -68,16 +73,22 @@ def main():
     ap.add_argument('--iterations', type=int, default=24)
     ap.add_argument('--games', type=int, default=512)
     ap.add_argument('--sims', type=int, default=32)
+    ap.add_argument('--min-iteration', type=int, default=19)
     ap.add_argument('--min-trunk', type=float, default=1000.0)
+    ap.add_argument('--min-spread', type=float, default=10.0)
+    ap.add_argument('--max-logit', type=float, default=1000.0)
     ap.add_argument('--save', default='')
-    ap.add_argument('--save-lr', type=float, default=None)
     args = ap.parse_args()
     from minitchess_alphazero_amd.build import build
     build(verbose=False)
     from minitchess_alphazero_amd.loop import run_loop
     dev = torch.device('cuda', 0)
     torch.use_deterministic_algorithms(False)
-    summary, finals = [], {}
+    summary, found = [], {}
+
+    class Done(Exception):
+        pass
+
     for lr in [float(x) for x in args.lrs.split(',')]:
         t0 = time.time()
         last = {}
@@ -86,27 +97,30 @@ def main():
             m = measure(net, rec, dev)
             m.update({'lr': lr, 'iteration': it, 'loss': h['loss'], 'plies_per_game': h['plies_per_game'],
                       'elapsed_s': round(time.time() - t0, 1)})
+            m['qualifies'] = (it >= args.min_iteration and m['trunk_max'] >= args.min_trunk
+                              and m['spread_max'] >= args.min_spread and m['logit_absmax'] <= args.max_logit)
             last.clear()
             last.update(m)
             print(json.dumps(m), flush=True)
+            if m['qualifies']:
+                found[lr] = {k: v.detach().cpu().clone().contiguous() for k, v in net.state_dict().items()}
+                raise Done()
 
-        _hist, net = run_loop(args.iterations, args.games, args.sims, lr=lr, device=0, log=lambda s: None,
-                              on_iteration=on_it)
-        finals[lr] = {k: v.detach().cpu().clone().contiguous() for k, v in net.state_dict().items()}
-        ok = (last['trunk_max'] >= args.min_trunk and last['spread_max'] >= 10 and last['value_std'] >= 0.05)
-        summary.append(dict(last, meets=ok))
-    pick = args.save_lr
-    if pick is None:
-        for s in summary:
-            if s['meets']:
-                pick = s['lr']
-                break
-    out = {'summary': summary, 'picked_lr': pick, 'iterations': args.iterations, 'games': args.games,
-           'sims': args.sims}
+        try:
+            run_loop(args.iterations, args.games, args.sims, lr=lr, device=0, log=lambda s: None, on_iteration=on_it)
+        except Done:
+            pass
+        summary.append(dict(last))
+        if found:
+            break
+    pick = next(iter(found), None)
+    out = {'summary': summary, 'picked_lr': pick, 'iterations_max': args.iterations, 'games': args.games,
+           'sims': args.sims, 'criteria': {'min_iteration': args.min_iteration, 'min_trunk': args.min_trunk,
+                                           'min_spread': args.min_spread, 'max_logit': args.max_logit}}
     if pick is not None and args.save:
         from safetensors.torch import save_file
         os.makedirs(os.path.dirname(os.path.abspath(args.save)), exist_ok=True)
-        save_file(finals[pick], args.save)
+        save_file(found[pick], args.save)
         out['saved'] = args.save
     print(json.dumps(out), flush=True)
 
