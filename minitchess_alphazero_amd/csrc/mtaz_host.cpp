@@ -1260,7 +1260,8 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
 
 // Variants a product library accepts: each parity-green against the reference fixtures
 // (tests/test_gpu_net.py).  k_net_y: 1024 = unfused epilogue (bit-identity reference).  k_net_z:
-// 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms,
+// 1 = the product kernel with 4 boards per workgroup in every round (no tail launches; bit-identity
+// reference and A/B for the tail-balanced assignment), 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms,
 // 25165824 = the round-2 K loop (per-step fragment addresses, global-address weights; bit-identity
 // reference for the product's tap-major loop), 33554432 = the round-2 epilogue (unscaled
 // conversions), 58720256 = both (the round-2 product).  The
@@ -1278,8 +1279,8 @@ extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
   if (h->precision == NET_F16X3) ok = ok || variant == 1024;
   if (h->precision == NET_F16F8)
-    ok = ok || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 || variant == 33554432 ||
-              variant == 8388608 + 16777216 + 33554432;
+    ok = ok || variant == 1 || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 ||
+         variant == 33554432 || variant == 8388608 + 16777216 + 33554432;
 #ifdef MTAZ_NET_DIAG
   ok = true;
 #endif

@@ -104,15 +104,18 @@ __device__ __forceinline__ uint32_t pk_fp8x4(float a, float b, float c, float d)
 // 2(w>>2) + 1: the same 16 accumulator tiles per wave with half the LDS bytes per MFMA and twice
 // the weight loads; bit-identical results, 3% more cycles at a 5% lower clock.
 // VAR 2048: 4 waves of 64 channels on all 4 boards.
-template <int VAR>
+// NVB: boards the workgroup computes (4; 1..3 in the tail launches, see k_net_z): boards
+// NVB..3 of the LDS image are never computed.
+template <int VAR, int NVB = XB>
 struct ZCfg {
   static constexpr bool BP = (VAR & 4194304) != 0;
   static constexpr int NW = (VAR & 2048) ? 4 : 8;   // waves
-  static constexpr int BPW = BP ? 2 : XB;           // boards per wave
+  static constexpr int NBG = BP ? 2 : 1;            // board groups
+  static constexpr int BPW = BP ? 2 : NVB;          // boards per wave
   static constexpr int CT = BP ? 4 : 16 / NW;       // channel tiles (of 16) per wave
   static constexpr int NCG = 16 / CT;               // channel groups
   static constexpr int TW = 2 * BPW;                // column tiles (board x square tile) per wave
-  static_assert(NCG * (XB / BPW) == NW, "waves cover channel groups x board groups");
+  static_assert(NCG * NBG == NW && (BP ? NVB == XB : NVB >= 1 && NVB <= XB), "waves cover channel groups x board groups");
 };
 
 // element bb of a 4-board register array with a wave-uniform runtime index, without a
@@ -122,13 +125,23 @@ __device__ __forceinline__ T pick4(const T* a, int bb) {
   return bb == 0 ? a[0] : bb == 1 ? a[1] : bb == 2 ? a[2] : a[3];
 }
 
-template <bool STAMP, int VAR>
+// Board assignment.  One workgroup holds a CU (its LDS image), so a launch runs in rounds of ncu
+// workgroups; with 4 boards each, n boards took ceil(n / 4 ncu) rounds and the last one was often
+// mostly idle (3,327 leaves: 832 workgroups, a fourth round with 64 of 256 CUs busy).  With
+// ncu > 0 the R = n mod 4 ncu boards beyond the full rounds need per = ceil(R / ncu) boards per
+// CU; if per < 4 they go to the tail launch k_net_z<NVB = per> instead, ceil(R / per) workgroups
+// that compute only their NVB boards, so the last round takes the time of its fewer boards per CU
+// (launch_net_z launches NVB = 1, 2, 3 after the full-round launch; the two that do not match exit
+// at once).  A board's result does not depend on the other boards of its workgroup (per-board e4m3
+// scales), so the assignment changes nothing but the time.  ncu = 0: 4 boards per workgroup
+// throughout (the other builds, the stamped diagnostics).
+template <bool STAMP, int VAR, int NVB = XB>
 __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                                  const int32_t* __restrict__ count, int max_b,
                                                                  int mode, float* __restrict__ logits_out,
                                                                  float* __restrict__ values_out,
-                                                                 unsigned long long* __restrict__ stamps) {
-  using C = ZCfg<VAR>;
+                                                                 unsigned long long* __restrict__ stamps, int ncu) {
+  using C = ZCfg<VAR, NVB>;
   constexpr int NW = C::NW, NT = 64 * NW, CT = C::CT, BPW = C::BPW, TW = C::TW;
   constexpr bool F6 = (VAR & 8192) != 0;   // cross terms in e2m3 blocks (epilogue6, NetWeights::conv6)
   // diagnostic builds (timing only, wrong results): 16384 = every layer reads layer 0's weights
@@ -164,8 +177,19 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   constexpr bool TAPA = (VAR & 8388608) == 0 && !DIAG_NOLDS && 8 % RA0 == 0;
   constexpr bool WBUF = (VAR & 16777216) == 0 && !F6;
   __shared__ __attribute__((aligned(16))) char smem[ZIMGB + AUXB];
-  const int nb = count ? *count : max_b;
-  const int b0 = blockIdx.x * XB;
+  int b0, nb;
+  {
+    const int n = count ? *count : max_b;
+    const int r = ncu > 0 ? n % (XB * ncu) : 0, per = ncu > 0 ? (r + ncu - 1) / ncu : XB;
+    if constexpr (NVB == XB) {   // the full rounds (and a tail of 4 boards per CU)
+      b0 = blockIdx.x * XB;
+      nb = per < XB ? n - r : n;
+    } else {                     // the tail, when it has NVB boards per CU
+      if (per != NVB) return;
+      b0 = n - r + blockIdx.x * NVB;
+      nb = b0 + NVB < n ? b0 + NVB : n;
+    }
+  }
   if (b0 >= nb) return;
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, n = lane & 15, g = lane >> 4;
@@ -882,7 +906,7 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
 #define Z_LAUNCH(V, T)                                                                                       \
-  hipLaunchKernelGGL((k_net_z<S, V>), grid, dim3(T), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps)
+  hipLaunchKernelGGL((k_net_z<S, V>), grid, dim3(T), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0)
   // product builds (mtaz_set_net_variant accepts these): 0, the unfused epilogue, e2m3 cross terms,
   // the round-2 K loop (per-step addresses, global-address weights)
   if (var == 2097152) Z_LAUNCH(2097152, 512);
@@ -914,13 +938,39 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
 #undef Z_LAUNCH
 }
 
+// compute units of the current device (the size of a launch's round)
+static int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cached[dev] = n > 0 ? n : -1;
+  }
+  return cached[dev] > 0 ? cached[dev] : 0;
+}
+
 void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
                   float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
                   int variant) {
   if (max_b <= 0) return;
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
-  launch_z<false>(variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode, logits_out, values_out,
-                  nullptr);
+  const int ncu = device_cus();
+  if (variant == 0 && ncu > 0) {   // the product: full rounds, then the tail launches (k_net_z above)
+    const dim3 blk(64 * ZCfg<0>::NW);
+    hipLaunchKernelGGL((k_net_z<false, 0, XB>), dim3((max_b + XB - 1) / XB), blk, 0, s, d, w, pos, count, max_b, mode,
+                       logits_out, values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_z<false, 0, 1>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_z<false, 0, 2>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_z<false, 0, 3>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+  } else {   // variant 1: the product kernel with 4 boards per workgroup throughout (the round-2 assignment)
+    launch_z<false>(variant == 1 ? 0 : variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode,
+                    logits_out, values_out, nullptr);
+  }
   if (ev_end) (void)hipEventRecord(ev_end, s);
 }
 

@@ -101,7 +101,8 @@ class Engine:
     def set_net_variant(self, variant):
         """Select a parity-tested build of the current precision's network kernel (0 = product;
         set_precision resets it).  f16x3 (k_net_y): 1024 = the epilogue in unfused form.  f16f8
-        (k_net_z): 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross terms,
+        (k_net_z): 1 = 4 boards per workgroup in every round (no tail launches), 2097152 = the
+        epilogue in unfused form, 8192 = e2m3 (fp6) cross terms,
         25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),
         33554432 = the round-2 epilogue (unscaled conversions), 58720256 = both (the round-2
         product); all but 8192 bitwise equal to 0.  Other values are rejected; the A/B and timing-only diagnostic builds exist only in

@@ -176,6 +176,32 @@ def test_z_loop_forms_bit_identical():
         assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
 
 
+@pytest.mark.parametrize('net_kind', ['seed0', 'wide', 'tiny'])
+def test_z_tail_launches_bit_identical(net_kind):
+    """The tail-balanced board assignment (k_net_z: the boards beyond the full rounds of 4 x CUs go
+    to workgroups of 1, 2 or 3 boards) computes every board exactly as 4 boards per workgroup do
+    (variant 1): batch sizes whose tails take each of the three tail builds and none."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from minitchess_alphazero_amd.network import Network
+    from tests_positions import random_fens
+    import torch
+    torch.manual_seed(0)
+    net = {'seed0': Network, 'wide': _wide_range_net, 'tiny': _tiny_activation_net}[net_kind]()
+    fens = random_fens(400, seed=29)
+    eng = Engine(n_games=4096, sims=4)
+    eng.set_precision('f16f8')
+    eng.set_weights(net)
+    for n in (1024 + 100, 1024 + 400, 1024 + 700, 2048 + 900, 37):
+        pos = np.stack([pos_from_fen(fens[i % len(fens)]) for i in range(n)])
+        eng.set_net_variant(0)
+        l0, v0 = eng.evaluate(pos)
+        eng.set_net_variant(1)
+        l1, v1 = eng.evaluate(pos)
+        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), n
+        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), n
+
+
 def _tiny_activation_net(scale=2.0 ** -20):
     """Random-init net with every BatchNorm gamma and beta x `scale` (stem and both convs of every
     block): folded weights and biases shrink with it, so the trunk's activations sit around
