@@ -50,7 +50,7 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
 #define YMMA(SA, SB, WP, XP)                                                                          \
   {                                                                                                   \
     _Pragma("unroll") for (int ct_ = 0; ct_ < CT; ++ct_)                                              \
-    _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_)                                                  \
+    _Pragma("unroll") for (int t_ = 0; t_ < 2 * NVB; ++t_)                                            \
       acc[ct_ * 8 + t_] = __builtin_amdgcn_mfma_f32_16x16x32_f16(SA[2 * ct_ + (WP)], SB[(XP) * 8 + t_], \
                                                                  acc[ct_ * 8 + t_], 0, 0, 0);         \
   }
@@ -61,14 +61,31 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
 // product's v_fma_mix epilogue, test_gpu_net.py).  Round 1's schedule A/B variants (whole-k-block
 // steps, sched_group_barrier interleaves, 8 waves of 32 channels) measured within 1% of the
 // pinned half-steps and were retired.
-template <bool STAMP, int VAR>
+// NVB / ncu: the tail-balanced board assignment of k_net_z (mtaz_net8.hip): with ncu > 0 the
+// NVB = 4 launch computes the full rounds of 4 boards per workgroup and the NVB = 1..3 launches
+// the remaining boards, at most NVB per workgroup, computing only those (boards NVB..3 of the
+// image are never computed).  The workgroup's stored-units exponent xs follows the bound of its
+// own boards, so the assignment is exact for any net whose activations stay below 2^14 (xs = 0).
+template <bool STAMP, int VAR, int NVB = XB>
 __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
                                                   const int32_t* __restrict__ count, int max_b, int mode,
                                                   float* __restrict__ logits_out, float* __restrict__ values_out,
-                                                  unsigned long long* __restrict__ stamps) {
+                                                  unsigned long long* __restrict__ stamps, int ncu) {
+  static_assert(NVB >= 1 && NVB <= XB, "boards per workgroup");
   __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
-  const int nb = count ? *count : max_b;
-  const int b0 = blockIdx.x * XB;
+  int b0, nb;
+  {
+    const int n = count ? *count : max_b;
+    const int r = ncu > 0 ? n % (XB * ncu) : 0, per = ncu > 0 ? (r + ncu - 1) / ncu : XB;
+    if constexpr (NVB == XB) {   // the full rounds (and a tail of 4 boards per CU)
+      b0 = blockIdx.x * XB;
+      nb = per < XB ? n - r : n;
+    } else {                     // the tail, when it has NVB boards per CU
+      if (per != NVB) return;
+      b0 = n - r + blockIdx.x * NVB;
+      nb = b0 + NVB < n ? b0 + NVB : n;
+    }
+  }
   if (b0 >= nb) return;
   constexpr int NW = 4, NT = 64 * NW, CT = 16 / NW;   // waves, threads, channel tiles per wave
   const int tid = threadIdx.x;
@@ -133,7 +150,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       const float4 bu = *reinterpret_cast<const float4*>(bias + co0);
       const float4 bv = make_float4(bu.x * st, bu.y * st, bu.z * st, bu.w * st);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < 2 * NVB; ++t) {
         const int bb = t >> 1, pt = t & 1;
         f32x4v& a = acc[ct * 8 + t];
         if (pt == 0 || p1 < 30) {
@@ -216,7 +233,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
 #pragma unroll
       for (int part = 0; part < 2; ++part)
 #pragma unroll
-        for (int bb = 0; bb < XB; ++bb) {
+        for (int bb = 0; bb < NVB; ++bb) {
           SB[part * 8 + 2 * bb] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r0) * 16);
           SB[part * 8 + 2 * bb + 1] = *reinterpret_cast<const f16x8*>(simg + ((part * XB + bb) * IROWS + r1) * 16);
         }
@@ -254,7 +271,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     const int r_ = (PT) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);   \
     const int o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                \
     _Pragma("unroll") for (int part_ = 0; part_ < 2; ++part_)                         \
-    _Pragma("unroll") for (int bb_ = 0; bb_ < XB; ++bb_)                              \
+    _Pragma("unroll") for (int bb_ = 0; bb_ < NVB; ++bb_)                             \
       S[part_ * 4 + bb_] = *reinterpret_cast<const f16x8*>(smem + part_ * PARTB + bb_ * IROWS * RB + o_); \
   }
 // product half-step: 12 chunks of 4 MFMAs in fixed program order (sched_barrier between
@@ -277,7 +294,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         const int g0_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 4 : 0;                        \
         const int g1_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 3 : 0;                        \
         _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_)                              \
-          if (q_ >= l0_ && q_ < l1_)                                                  \
+          if (q_ >= l0_ && q_ < l1_ && (q_ & 3) < NVB)                                \
             BN[q_] = *reinterpret_cast<const f16x8*>(smem + (q_ >> 2) * PARTB + (q_ & 3) * IROWS * RB + o_); \
         _Pragma("unroll") for (int q_ = 0; q_ < CT; ++q_)                             \
           if (q_ >= g0_ && q_ < g1_) {                                                \
@@ -288,8 +305,9 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       }                                                                               \
       const int ps_ = i_ / (4 * CT), ct_ = (i_ >> 2) % CT, bb_ = i_ & 3;              \
       const int wp_ = ps_ == 2 ? 1 : 0, xp_ = ps_ == 1 ? 1 : 0;                       \
-      acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(         \
-          AC[2 * ct_ + wp_], BC[xp_ * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0); \
+      if (bb_ < NVB)                                                                  \
+        acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(       \
+            AC[2 * ct_ + wp_], BC[xp_ * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0); \
     }                                                                                 \
     __builtin_amdgcn_sched_barrier(0);                                                \
   }
@@ -344,9 +362,21 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      const int32_t* count, int max_b, int mode, float* logits, float* values,
                      unsigned long long* stamps) {
   if (var == 1024)
-    hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+    hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else
-    hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps);
+    hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+}
+
+static int device_cus_y() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cached[dev] = n > 0 ? n : -1;
+  }
+  return cached[dev] > 0 ? cached[dev] : 0;
 }
 
 void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
@@ -354,8 +384,20 @@ void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const i
                   int variant) {
   if (max_b <= 0) return;
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
-  launch_y<false>(variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode, logits_out, values_out,
-                  nullptr);
+  const int ncu = device_cus_y();
+  if (variant == 0 && ncu > 0) {   // the product: full rounds, then the tail launches (k_net_y above)
+    hipLaunchKernelGGL((k_net_y<false, 0, XB>), dim3((max_b + XB - 1) / XB), dim3(256), 0, s, d, w, pos, count, max_b,
+                       mode, logits_out, values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_y<false, 0, 1>), dim3(ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_y<false, 0, 2>), dim3(ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_y<false, 0, 3>), dim3(ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+  } else {   // variant 1: 4 boards per workgroup throughout
+    launch_y<false>(variant == 1 ? 0 : variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode,
+                    logits_out, values_out, nullptr);
+  }
   if (ev_end) (void)hipEventRecord(ev_end, s);
 }
 
