@@ -28,10 +28,10 @@ mkdir -p "$OUT"
 run() {   # name timeout command...
   local name=$1 lim=$2
   shift 2
-  echo "[gpu.sh] $name: $*"
+  echo "[gpu.sh] $name: $*" >&2
   timeout -k 10 "$lim" "$@"
   local rc=$?
-  echo "[gpu.sh] $name rc=$rc"
+  echo "[gpu.sh] $name rc=$rc" >&2
   return $rc
 }
 

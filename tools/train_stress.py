@@ -17,11 +17,15 @@ self-play kernels fold) on up to 2,048 positions of that iteration's self-play:
   value_std     std of the value over the positions (a collapsed value head has ~0)
 A network qualifies after update >= --min-iteration (the verdict asks for >= 20 updates) when
 trunk_max >= --min-trunk (activations in the thousands), spread_max >= --min-spread (peaked
-priors) and the largest |logit| <= --max-logit (beyond that, fp32's own rounding of the logits
-exceeds the 1e-5 prior budget, so no fp32 implementation could match another to it).  For each
-learning rate the loop stops at the first qualifying network; the first learning rate that
-produced one is saved (--save, safetensors).  GPU training is not bitwise reproducible, so the
-saved checkpoint is data: tests/golden/make_golden_r3.py pins it by sha256.
+priors) and the largest |logit| <= --max-logit (the runs pass through transient blow-ups with
+logits of 1e5 and more, where fp32's own rounding of a logit exceeds the 1e-5 prior budget; the
+cap keeps the checkpoint in the regime the parity bound can speak about).  The selection looks at
+these stress measures only, never at how the kernels do on the network.  For each learning rate
+the loop stops at the first qualifying network; the first learning rate that produced one is
+saved (--save, safetensors), with, for information, the largest prior / value deviation of the
+GPU network builds from the CPU fp32 network (the oracle's restatement of exp/policy.py) on 256
+of its positions.  GPU training is not bitwise reproducible, so the saved checkpoint is data:
+tests/golden/make_golden_r3.py pins it by sha256 and records the reference's outputs on it.
 Output: one JSON line per iteration on stdout, a summary line at the end.
 """
 import argparse
@@ -67,6 +71,41 @@ def measure(net, rec, device, max_pos=2048):
             'value_max': float(value.max()), 'logit_absmax': float(np.abs(logits).max()), 'positions': int(n)}
 
 
+def deviation(sd, rec, n=256):
+    """max |P - P_cpu| (softmax over the legal list) and |v - v_cpu| of k_net_z and k_net_y against
+    the CPU fp32 forward (oracle.net, the reference's torch ops) on n positions of `rec`."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_to_fen
+    from oracle.encoder import process_observation
+    from oracle.net import Network as RefNet
+    ref = RefNet()
+    ref.load_state_dict(sd)
+    ref.eval()
+    idx = np.linspace(0, len(rec) - 1, min(n, len(rec))).astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(rec.k)[:-1]])
+    out = {}
+    cpu = []
+    with torch.no_grad():
+        for i in idx:
+            p, v = ref(process_observation(pos_to_fen(rec.pos[i])))
+            cpu.append((p[0].double().numpy(), float(v.item())))
+    for prec in ('f16f8', 'f16x3'):
+        eng = Engine(n_games=len(idx), sims=2)
+        eng.set_precision(prec)
+        eng.set_weights(sd)
+        lg, vals = eng.evaluate(rec.pos[idx])
+        dp = dv = 0.0
+        for j, i in enumerate(idx):
+            codes = rec.codes[starts[i]:starts[i] + rec.k[i]].astype(np.int64)
+            a = torch.from_numpy(lg[j][codes]).softmax(0).double().numpy()
+            b = torch.from_numpy(cpu[j][0][codes]).float().softmax(0).double().numpy()
+            dp = max(dp, float(np.max(np.abs(a - b))))
+            dv = max(dv, abs(float(vals[j]) - cpu[j][1]))
+        out[prec] = {'max_dP': dp, 'max_dv': dv}
+        eng.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--lrs', default='0.003,0.01,0.03')
@@ -76,7 +115,7 @@ def main():
     ap.add_argument('--min-iteration', type=int, default=19)
     ap.add_argument('--min-trunk', type=float, default=1000.0)
     ap.add_argument('--min-spread', type=float, default=10.0)
-    ap.add_argument('--max-logit', type=float, default=1000.0)
+    ap.add_argument('--max-logit', type=float, default=3000.0)
     ap.add_argument('--save', default='')
     args = ap.parse_args()
     from minitchess_alphazero_amd.build import build
@@ -84,7 +123,7 @@ def main():
     from minitchess_alphazero_amd.loop import run_loop
     dev = torch.device('cuda', 0)
     torch.use_deterministic_algorithms(False)
-    summary, found = [], {}
+    summary, found, last_rec = [], {}, [None]
 
     class Done(Exception):
         pass
@@ -94,6 +133,7 @@ def main():
         last = {}
 
         def on_it(it, net, rec, h):
+            last_rec[0] = rec
             m = measure(net, rec, dev)
             m.update({'lr': lr, 'iteration': it, 'loss': h['loss'], 'plies_per_game': h['plies_per_game'],
                       'elapsed_s': round(time.time() - t0, 1)})
@@ -122,6 +162,7 @@ def main():
         os.makedirs(os.path.dirname(os.path.abspath(args.save)), exist_ok=True)
         save_file(found[pick], args.save)
         out['saved'] = args.save
+        out['deviation_vs_cpu_fp32'] = deviation(found[pick], last_rec[0])
     print(json.dumps(out), flush=True)
 
 
