@@ -252,7 +252,7 @@ def main():
             dist.barrier()
 
     KEYS = ('sims', 'nn_evals', 'memo_hits', 'memo_batch_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
-            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms')
+            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms', 'choice_ms', 'gap_ms')
 
     def timed(engine, steps, label):
         """`steps` full self-play batches between barrier + synchronize; max wall over ranks and
@@ -371,6 +371,10 @@ def main():
                           'leaf_compact_avg_ms': tot['compact_ms'] / tot['waves'] if tot['waves'] else None},
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
+        # host time between two moves' simulations (the GPU idles): action choice + records
+        # (host_choice_s), apply, game states, move start, the first Dirichlet draws
+        'host_gap_s': tot['gap_ms'] / 1e3,
+        'host_choice_s': tot['choice_ms'] / 1e3,
     }
     if secondary is not None:
         line['secondary'] = secondary

@@ -440,17 +440,35 @@ extern "C" int mtaz_encode_batch(int device, const uint32_t* d_pos, int n, uint8
 // ---------------------------------------------------------------------------------------
 // engine
 namespace {
-struct PlyRec {
-  Pos pos;
-  int32_t action;
+// One game's InfoRecorder records (exp/callbacks.py:40-47): per ply the observation, the action
+// and its legal list length; the legal codes and root visit counts of all plies concatenated
+// (no allocation per ply: the vectors keep their capacity across plays).
+struct GameRec {
+  std::vector<Pos> pos;
+  std::vector<int32_t> action, k;
   std::vector<uint16_t> codes;
   std::vector<uint32_t> visits;
+  size_t plies() const { return pos.size(); }
+  void clear() {
+    pos.clear();
+    action.clear();
+    k.clear();
+    codes.clear();
+    visits.clear();
+  }
+  void add(const Pos& p, int32_t a, const uint16_t* c, const uint32_t* v, int kk) {
+    pos.push_back(p);
+    action.push_back(a);
+    k.push_back(kk);
+    codes.insert(codes.end(), c, c + kk);
+    visits.insert(visits.end(), v, v + kk);
+  }
 };
 
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
-  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_COUNT
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_CHOICE_MS, ST_GAP_MS, ST_COUNT
 };
 
 // Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
@@ -614,7 +632,7 @@ struct mtaz_engine {
   size_t noise_host_cap = 0;
   std::vector<int32_t> last_root_k;     // root legal counts of the last mtaz_move_begin
   std::vector<MTState> rng;
-  std::vector<std::vector<PlyRec>> rec;
+  std::vector<GameRec> rec;
   std::vector<int32_t> final_outcome;
   int n_played = 0;
   double stats[ST_COUNT] = {0};
@@ -1778,12 +1796,13 @@ static int play_groups(mtaz_engine* h) {
   h->group_pool->run(ng, body);
   for (int i = 0; i < ng; ++i)
     if (rc[i] < 0) return set_err(rc[i], "group %d: %s", i, err[i].c_str());
-  h->rec.clear();
+  h->rec.resize(h->G);
   h->final_outcome.clear();
   for (int i = 0; i < ST_COUNT; ++i) h->stats[i] = 0;
   h->wave = 0;
-  for (mtaz_engine* p : h->parts) {
-    for (auto& r : p->rec) h->rec.push_back(std::move(r));
+  for (int pi = 0; pi < ng; ++pi) {
+    mtaz_engine* p = h->parts[pi];
+    for (int gi = 0; gi < Gp; ++gi) std::swap(h->rec[(size_t)pi * Gp + gi], p->rec[gi]);
     h->final_outcome.insert(h->final_outcome.end(), p->final_outcome.begin(), p->final_outcome.end());
     for (int i = 0; i < ST_COUNT; ++i) {
       if (i == ST_MAX_NODES || i == ST_MAX_EDGES || i == ST_NET_PREC || i == ST_MOVES)
@@ -1828,7 +1847,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   }
   ECHK(mtaz_clear_trees(h, nullptr, 0));
   for (int g = 0; g < G; ++g) mt_seed(h->rng[g], (uint32_t)(h->seed_base + (uint64_t)g));
-  h->rec.assign(G, {});
+  h->rec.resize(G);
+  for (auto& r : h->rec) r.clear();
   h->final_outcome.assign(G, 0);
   h->wave = 0;
   h->n_played = n_games;
@@ -1841,7 +1861,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   std::vector<uint16_t> codes((size_t)G * KMAX);
   std::vector<uint32_t> visits((size_t)G * KMAX);
   ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
-  double rng_ms = 0, sync_ms = 0;
+  double rng_ms = 0, sync_ms = 0, choice_ms = 0, gap_ms = 0;
+  double t_gap = -1;   // when the last move's root visit counts reached the host
   int moves = 0;
   for (;;) {
     int n_active = 0;
@@ -1898,6 +1919,9 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     };
     ECHK(draw_chunk(0));
     rng_ms += now_ms() - tr;
+    // host time between two moves' simulations: action choice, apply, game states, move start,
+    // the first chunk of Dirichlet draws (the GPU idles meanwhile)
+    if (t_gap >= 0) gap_ms += now_ms() - t_gap;
     for (int s0 = 0; s0 < h->sims; s0 = chunk_end(s0)) {
       // simulation s uses draw s - root_new <= s: the chunk holding draw s is on the stream first
       for (int s = s0; s < chunk_end(s0); ++s) ECHK(sim_gpu(h, s));
@@ -1914,6 +1938,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     ts = now_ms();
     ECHK(mtaz_move_end(h, codes.data(), visits.data(), nullptr, kmx));
     sync_ms += now_ms() - ts;
+    t_gap = now_ms();
     // action selection (exp/agent.py:110-119) + records (exp/callbacks.py:40-47)
     tr = now_ms();
     parallel_for(G, h->host_threads, [&](int g) {
@@ -1938,14 +1963,10 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
         idx = maxima[legacy_randint(h->rng[g], m)];
       }
       actions[g] = c[idx];
-      PlyRec r;
-      r.pos = pos_in(&roots[5 * g]);
-      r.action = c[idx];
-      r.codes.assign(c, c + k);
-      r.visits.assign(v, v + k);
-      h->rec[g].push_back(std::move(r));
+      h->rec[g].add(pos_in(&roots[5 * g]), c[idx], c, v, k);
     });
     rng_ms += now_ms() - tr;
+    choice_ms += now_ms() - tr;
     ts = now_ms();
     ECHK(mtaz_apply(h, actions.data()));
     ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
@@ -1981,7 +2002,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   }
   int64_t plies = 0, decisive = 0;
   for (int g = 0; g < n_games; ++g) {
-    plies += (int64_t)h->rec[g].size();
+    plies += (int64_t)h->rec[g].plies();
     decisive += h->final_outcome[g] == DECISIVE;
   }
   // largest table of the batch (device error flags already guard the capacities)
@@ -2016,6 +2037,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_SYNC_MS] = sync_ms;
   h->stats[ST_NET_PREC] = h->precision;
   h->stats[ST_SELECT_MS] = select_ms;
+  h->stats[ST_CHOICE_MS] = choice_ms;
+  h->stats[ST_GAP_MS] = gap_ms;
   h->stats[ST_COMPACT_MS] = compact_ms;
   return 0;
 }
@@ -2031,9 +2054,9 @@ extern "C" int mtaz_stats(mtaz_engine* h, double* out, int n) {
 extern "C" int mtaz_records_counts(mtaz_engine* h, int32_t* plies_per_game, int64_t* total_plies, int64_t* total_entries) {
   int64_t tp = 0, te = 0;
   for (int g = 0; g < h->n_played; ++g) {
-    plies_per_game[g] = (int32_t)h->rec[g].size();
-    tp += (int64_t)h->rec[g].size();
-    for (auto& r : h->rec[g]) te += (int64_t)r.codes.size();
+    plies_per_game[g] = (int32_t)h->rec[g].plies();
+    tp += (int64_t)h->rec[g].plies();
+    te += (int64_t)h->rec[g].codes.size();
   }
   *total_plies = tp;
   *total_entries = te;
@@ -2049,21 +2072,19 @@ extern "C" int mtaz_records_get(mtaz_engine* h, uint32_t* pos, int32_t* action, 
     const auto& R = h->rec[g];
     const int oc = h->final_outcome[g];
     if (outcome_out) outcome_out[g] = oc;
-    float rw = oc == DECISIVE ? 1.0f : 0.0f;
-    std::vector<float> rws(R.size());
-    for (int i = (int)R.size() - 1; i >= 0; --i) {
-      rws[i] = rw;
+    const int np = (int)R.plies();
+    // the last ply's reward is the game's (1 decisive, 0 draw), alternating in sign towards ply 0
+    float rw = ((np - 1) & 1) ? -(oc == DECISIVE ? 1.0f : 0.0f) : (oc == DECISIVE ? 1.0f : 0.0f);
+    for (int i = 0; i < np; ++i, ++p) {
+      pos_out(R.pos[i], pos + 5 * p);
+      action[p] = R.action[i];
+      k[p] = R.k[i];
+      reward[p] = rw;
       rw = -rw;
     }
-    for (size_t i = 0; i < R.size(); ++i, ++p) {
-      pos_out(R[i].pos, pos + 5 * p);
-      action[p] = R[i].action;
-      k[p] = (int32_t)R[i].codes.size();
-      reward[p] = rws[i];
-      memcpy(codes + e, R[i].codes.data(), R[i].codes.size() * 2);
-      memcpy(visits + e, R[i].visits.data(), R[i].visits.size() * 4);
-      e += (int64_t)R[i].codes.size();
-    }
+    memcpy(codes + e, R.codes.data(), R.codes.size() * 2);
+    memcpy(visits + e, R.visits.data(), R.visits.size() * 4);
+    e += (int64_t)R.codes.size();
   }
   return 0;
 }

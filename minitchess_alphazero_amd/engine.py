@@ -25,7 +25,7 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
               'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap',
-              'memo_batch_hits']
+              'memo_batch_hits', 'choice_ms', 'gap_ms']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
