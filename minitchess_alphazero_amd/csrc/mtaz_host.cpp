@@ -608,7 +608,10 @@ struct mtaz_engine {
   NetWeights w{};
   NetBuffers nb{};
   bool weights_ok = false;
-  int precision = NET_F16F8;   // k_net_z; NET_F16X3 = k_net_y (fp32-accurate to ~1e-8)
+  // k_net_y (fp16x3, fp32-accurate to ~1e-8): within the north_star's 1e-5 on every tested net,
+  // the round-3 stress checkpoint included; NET_F16F8 = k_net_z (e4m3 cross terms) is not within
+  // 1e-5 there (tests/test_gpu_stress.py), so it is an option, not the default
+  int precision = NET_F16X3;
   int variant = 0;   // network kernel variant of the current precision (0 = product; mtaz_set_net_variant)
   uint4* wxbuf = nullptr;
   float* wxinv = nullptr;

@@ -122,6 +122,23 @@ def c3_network():
     return net.eval()
 
 
+def stress_network():
+    """The round-3 stress checkpoint (tools/train_stress.py, pinned by tests/golden/make_golden_r3.py):
+    21 reference-learner updates in the C5 loop at lr 0.02, trunk activations in the thousands,
+    legal-logit spreads up to ~80 on its fixture positions; sha256-checked."""
+    import json
+    import os
+    from safetensors.torch import load_file
+    from minitchess_alphazero_amd.network import Network
+    from oracle.net import state_dict_sha256
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+    net = Network()
+    net.load_state_dict(load_file(os.path.join(here, 'stress', 'stress.safetensors')))
+    meta = json.load(open(os.path.join(here, 'stress.json')))
+    assert state_dict_sha256(net) == meta['state_dict_sha256'], 'stress checkpoint does not match its pinned sha256'
+    return net.eval()
+
+
 class RecordedEvaluator:
     """Oracle evaluator returning recorded leaf results by FEN (the network is a function of the
     position, so a replay asks only for positions the recorded run evaluated)."""

@@ -1,0 +1,147 @@
+"""GPU: the round-3 STRESS checkpoint: a network the reference learner's update
+drove to peaked priors and trunk activations in the thousands (tools/train_stress.py; 21 updates at
+lr 0.02 in the C5 loop).  The checkpoint is pinned by sha256 and the reference's own outputs on it
+come from tests/golden/make_golden_r3.py (the reference exp/policy.py Network.forward, eval mode, in
+the build container), with one 64-sim reference self-play game.
+
+  * network parity, the north_star bound for every product precision that claims it: priors
+    (softmax over the legal list) and values within 1e-5, logits within 1e-5 of each row's
+    largest |logit| (the fp32 error scale at these magnitudes);
+  * the priors and values the search consumes (device-written leaf results), same bound;
+  * L1: the reference's 64-sim game bit-exact with host leaves (batch-1 torch CPU);
+  * L3: the GPU network end to end, divergences only at near-ties the measured leaf deviations
+    explain (helpers.explain_divergence);
+  * k_net_z (f16f8) is NOT within 1e-5 here (its e4m3 cross terms carry ~2^-15 of each layer's
+    output; tools/split_error.py: any 8-bit cross term misses on this net): the engine's default
+    precision is k_net_y (f16x3), and test_f16f8_outside_its_scope_on_the_stress_net records the
+    measured deviation.
+The value head of this checkpoint has collapsed to a constant (-0.0117 on every position: the
+self-play data of the loop is almost all draws), so the value checks are weak here; the C3 net
+covers varying values."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+from helpers import compare_records, drive_engine, stress_network
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+EXACT = ['f16x3', 'fp32']          # the precisions whose north_star claim covers this net
+
+
+def _fixture():
+    z = np.load(os.path.join(GOLDEN, 'stress_net.npz'))
+    return [str(f) for f in z['fens']], z['logits'].astype(np.float64), z['values'].astype(np.float64)
+
+
+def _deviations(precision):
+    import torch
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen, pos_legal
+    fens, ref_l, ref_v = _fixture()
+    eng = Engine(n_games=len(fens), sims=4)
+    eng.set_precision(precision)
+    eng.set_weights(stress_network())
+    pos = np.stack([pos_from_fen(f) for f in fens])
+    logits, values = eng.evaluate(pos)
+    dl = float(np.max(np.abs(logits - ref_l) / np.maximum(1.0, np.abs(ref_l).max(axis=1, keepdims=True))))
+    dv = float(np.max(np.abs(values - ref_v)))
+    dp, dup = 0.0, 0
+    for i in range(len(fens)):
+        legal = pos_legal(pos[i])
+        if not legal:
+            continue
+        dup += len(set(legal)) < len(legal)
+        a = torch.from_numpy(logits[i][legal]).softmax(0).double().numpy()
+        b = torch.from_numpy(ref_l[i][legal].astype(np.float32)).softmax(0).double().numpy()
+        dp = max(dp, float(np.max(np.abs(a - b))))
+    return dl, dp, dv, dup
+
+
+def test_stress_checkpoint_pinned_and_stressed():
+    meta = load_golden('stress')
+    stress_network()
+    assert meta['trunk_absmax'] >= 1000 and meta['legal_logit_spread_max'] >= 10
+    assert meta['training']['summary']['criteria']['min_iteration'] >= 19     # >= 20 learner updates
+
+
+@pytest.mark.parametrize('precision', EXACT)
+def test_stress_net_vs_reference(precision):
+    dl, dp, dv, dup = _deviations(precision)
+    print(f'stress {precision}: logits {dl:.3e} of the row scale, priors {dp:.3e}, values {dv:.3e}; '
+          f'{dup} legal lists with repeated codes')
+    assert dl <= TOL and dp <= TOL and dv <= TOL
+
+
+def test_f16f8_outside_its_scope_on_the_stress_net():
+    """k_net_z's measured deviation on this net, recorded (gpurun_out/stress_scope.txt); the
+    engine's default network is k_net_y."""
+    from minitchess_alphazero_amd.engine import Engine
+    from conftest import REPO
+    dl, dp, dv, _ = _deviations('f16f8')
+    msg = f'k_net_z (f16f8) on the stress net: logits {dl:.3e} of the row scale, priors {dp:.3e}, values {dv:.3e}'
+    print(msg)
+    os.makedirs(os.path.join(REPO, 'gpurun_out'), exist_ok=True)
+    with open(os.path.join(REPO, 'gpurun_out', 'stress_scope.txt'), 'w') as fh:
+        fh.write(msg + '\n')
+    assert Engine.DEFAULT_PRECISION == 'f16x3'
+
+
+@pytest.mark.parametrize('precision', EXACT)
+def test_stress_leaf_priors_and_values(precision):
+    """The priors and values the search consumes on this net (device-written leaf results of
+    sim_evaluate) vs the reference's softmax over its own logits, repeated promotion codes kept."""
+    import torch
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen, pos_legal, pos_outcome
+    fens, ref_l, ref_v = _fixture()
+    roots = [i for i, f in enumerate(fens) if pos_legal(pos_from_fen(f)) and pos_outcome(pos_from_fen(f)) == 0]
+    eng = Engine(n_games=len(roots), sims=4)
+    eng.set_precision(precision)
+    eng.set_weights(stress_network())
+    eng.set_games([fens[i] for i in roots])
+    eng.clear_trees()
+    eng.move_begin()
+    eng.set_noise([None] * eng.G)
+    eng.sim_select(0)
+    _lpos, lgame, lk, lcodes = eng.leaves()
+    eng.sim_evaluate()
+    P, v = eng.leaf_results()
+    worst_p = worst_v = 0.0
+    for i in range(len(lgame)):
+        j = roots[int(lgame[i])]
+        legal = [int(c) for c in lcodes[i][:lk[i]]]
+        ref = torch.from_numpy(ref_l[j][legal].astype(np.float32)).softmax(0).double().numpy()
+        worst_p = max(worst_p, float(np.max(np.abs(P[i][:len(legal)].astype(np.float64) - ref))))
+        worst_v = max(worst_v, abs(float(v[i]) - float(ref_v[j])))
+    print(f'stress leaves {precision}: {len(lgame)} leaves, max |P - ref| {worst_p:.3e}, max |v - ref| {worst_v:.3e}')
+    assert worst_p <= TOL and worst_v <= TOL
+    eng.sim_backup()
+
+
+def test_stress_host_leaves_64_sims_equal_reference():
+    """L1 on the stress net: the reference's 64-sim game, leaves evaluated batch-1 on the host exactly
+    as exp/agent.py:66-69; every pi and action bit-exact."""
+    from minitchess_alphazero_amd.engine import Engine
+    from oracle.mcts import TorchNetEvaluator
+    from oracle.net import Network as RefNet
+    gm = load_golden('stress')['stress_64']
+    ref = RefNet()
+    ref.load_state_dict(stress_network().state_dict())
+    eng = Engine(n_games=1, sims=gm['sims'])
+    recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=TorchNetEvaluator(ref.eval()))
+    assert compare_records(recs[0], gm['moves'])[2] is None
+    assert [x['reward'] for x in recs[0]] == [x['reward'] for x in gm['moves']]
+
+
+@pytest.mark.parametrize('precision', EXACT[:1])
+def test_stress_gpu_net_64_sims_vs_reference(precision):
+    """L3 on the stress net with the default network (k_net_y)."""
+    from test_gpu_search_parity import _l3
+    from oracle.net import Network as RefNet
+    ref = RefNet()
+    ref.load_state_dict(stress_network().state_dict())
+    _l3('stress_64', precision, stress_network(), ref.eval(), [load_golden('stress')['stress_64']])
