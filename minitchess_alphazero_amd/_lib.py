@@ -105,6 +105,10 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise MtazLibraryError(f'{LIB_PATH} not built: run `python -m minitchess_alphazero_amd.build` '
                                '(the HIP extension is required; there is no CPU fallback)')
+    # torch's wheel carries its own HIP runtime under the same soname (libamdhip64.so.7) as
+    # /opt/rocm's: load torch first so that the process holds ONE runtime, the one torch was built
+    # against (libmtaz loaded first binds /opt/rocm's, and torch then finds no GPU)
+    import torch  # noqa: F401
     try:
         L = ctypes.CDLL(LIB_PATH)
     except OSError as e:

@@ -107,9 +107,17 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // the lane's output squares: n (tile 0) and p1 = 16 + n (tile 1; 30, 31 are padding)
   const int p1 = 16 + n;
   const int ph0 = n / 5, pw0 = n % 5, ph1 = p1 / 5, pw1 = p1 % 5;
-  f32x4v acc[CT * 8];
+  // VAR 4096 (CH): chunked accumulation.  The MFMAs of every U = 12 k-blocks accumulate from zero
+  // into acc, which is then added into the master sums mst (fp32, round to nearest; the next
+  // chunk's first MFMAs start from C = 0).  Each output takes 6 roundings at its full magnitude per
+  // layer instead of one per MFMA (216), and the residual (seeded into mst) no longer sits under
+  // every MFMA's rounding.  The epilogue reads mst + acc.
+  constexpr bool CH = (VAR & 4096) != 0;
+  f32x4v acc[CT * 8], mst[CH ? CT * 8 : 1];
 #pragma unroll
   for (int i = 0; i < CT * 8; ++i) acc[i] = (f32x4v){0};
+#pragma unroll
+  for (int i = 0; i < (CH ? CT * 8 : 1); ++i) mst[i] = (f32x4v){0};
   int overflow = 0;
 
   // Dynamic range.  The image holds x * 2^-xs in f16 hi/lo with one exponent xs per workgroup
@@ -152,7 +160,12 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
 #pragma unroll
       for (int t = 0; t < 2 * NVB; ++t) {
         const int bb = t >> 1, pt = t & 1;
-        f32x4v& a = acc[ct * 8 + t];
+        f32x4v& acc_t = acc[ct * 8 + t];
+        f32x4v& a = CH ? mst[CH ? ct * 8 + t : 0] : acc_t;   // the sum; the next layer's seed goes here
+        if constexpr (CH) {
+          a += acc_t;
+          acc_t = (f32x4v){0};
+        }
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
           const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1), al = ah + PARTB;
@@ -250,7 +263,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // activation fragments of one tile are live (a 2 x 8-fragment ring): the next half's are read
   // from LDS during the current half, in 12 chunks of 4 MFMAs whose order sched_barrier pins
   // (HALF_PINNED: no accumulator copies, no spills).
-  constexpr int PD = 2, RS = 3, U = 6;
+  constexpr int PD = 2, RS = 3, U = CH ? 12 : 6;
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
   f16x8 A[RS][2 * CT], BH[2][8];
   const uint4* Wl = W.convy + (size_t)(CT * wave) * KBY * 128 + lane;
@@ -321,6 +334,13 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         HALF_PINNED(kb + u, 0, A[u % RS], A[(u + PD) % RS], BH[0], BH[1], kb + u, 1);
         HALF_PINNED(kb + u, 1, A[u % RS], A[(u + PD) % RS], BH[1], BH[0], kb + u + 1, 0);
       }
+      if constexpr (CH) {   // the chunk into the master sums; the next chunk starts from C = 0
+#pragma unroll
+        for (int i = 0; i < CT * 8; ++i) {
+          mst[CH ? i : 0] += acc[i];
+          acc[i] = (f32x4v){0};
+        }
+      }
     }
     stamp(st_k);
     Wl += CONVX_U4_PER_LAYER;
@@ -363,6 +383,8 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      unsigned long long* stamps) {
   if (var == 1024)
     hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == 4096)
+    hipLaunchKernelGGL((k_net_y<S, 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else
     hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
 }

@@ -144,6 +144,12 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   using C = ZCfg<VAR, NVB>;
   constexpr int NW = C::NW, NT = 64 * NW, CT = C::CT, BPW = C::BPW, TW = C::TW;
   constexpr bool F6 = (VAR & 8192) != 0;   // cross terms in e2m3 blocks (epilogue6, NetWeights::conv6)
+  // 268435456 (W3): k_net_y's arithmetic (all three split products on the f16 MFMA, fp32-accurate)
+  // in this kernel's structure: part 1 of the image holds Xl = f16(y - Xh) instead of the e4m3
+  // copies, and each K step runs Wh*Xh and Wl*Xh on the step's Xh fragments, then Wh*Xl on its Xl
+  // fragments (Wl: the lo part of convz), 48 f16 MFMAs per wave and step
+  constexpr bool W3 = (VAR & 268435456) != 0;
+  static_assert(!(W3 && F6), "W3 has no e2m3 form");
   // diagnostic builds (timing only, wrong results): 16384 = every layer reads layer 0's weights
   // (an L2-resident weight set), 32768 = every step reads k-block / group 0 (L1-resident)
   constexpr bool DIAG_L2 = (VAR & 16384) != 0, DIAG_L1 = (VAR & 32768) != 0;
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   // Xh8 copies and the residual seed's Xl8 decode; -35% epilogue VALU).  33554432 = the round-2
   // form (v_fma_mix scalings, unscaled conversions); bit-identical (test_z_mix_epilogue_bit_identical
   // against the unfused form)
-  constexpr bool SCVT = (VAR & 33554432) == 0 && !NOMIX && !F6;   // (e2m3: more spills with it)
+  constexpr bool SCVT = (VAR & 33554432) == 0 && !NOMIX && !F6 && !W3;   // (e2m3: more spills with it)
   // K-loop form.  Product: tap-major (one tap = 8 steps per iteration; a fragment's LDS offset is a
   // per-tap base plus a step constant, selected against the zero cell by the tap's on-board mask,
   // 2-3 VALU per address) with the weight fragments by buffer loads (descriptor + per-wave lane
@@ -325,7 +331,19 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
           }
           ymax[j] = fmaxf(ymax[j], fmaxf(fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])),
                                          fmaxf(fmaxf(y[4], y[5]), fmaxf(y[6], y[7]))));
-          if constexpr (conv_a) {
+          if constexpr (conv_a && W3) {
+            // seed conv B with the block input Xh + Xl (both f16, part 0 / part 1), in conv B's units
+            const uint4 xp = *reinterpret_cast<const uint4*>(smem + ah);
+            const uint4 xq = *reinterpret_cast<const uint4*>(smem + ah + ZPART);
+            a0[0] = zmix_lo(xp.x, sseed, zmix_lo(xq.x, sseed, 0.f));
+            a0[1] = zmix_hi(xp.x, sseed, zmix_hi(xq.x, sseed, 0.f));
+            a0[2] = zmix_lo(xp.y, sseed, zmix_lo(xq.y, sseed, 0.f));
+            a0[3] = zmix_hi(xp.y, sseed, zmix_hi(xq.y, sseed, 0.f));
+            a1[0] = zmix_lo(xp.z, sseed, zmix_lo(xq.z, sseed, 0.f));
+            a1[1] = zmix_hi(xp.z, sseed, zmix_hi(xq.z, sseed, 0.f));
+            a1[2] = zmix_lo(xp.w, sseed, zmix_lo(xq.w, sseed, 0.f));
+            a1[3] = zmix_hi(xp.w, sseed, zmix_hi(xq.w, sseed, 0.f));
+          } else if constexpr (conv_a) {
             const uint2 xl = *reinterpret_cast<const uint2*>(smem + al8);
             if constexpr (NOMIX) {
               const f16x8 xh = *reinterpret_cast<const f16x8*>(smem + ah);
@@ -365,6 +383,20 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
           f16x8 yh;
 #pragma unroll
           for (int q = 0; q < 8; ++q) yh[q] = (_Float16)y[q];
+          if constexpr (W3) {
+            // part 0 <- Xh = f16(y), part 1 <- Xl = f16(y - Xh) (the difference is exact)
+            const uint4 yp = __builtin_bit_cast(uint4, yh);
+            const uint32_t yw[4] = {yp.x, yp.y, yp.z, yp.w};
+            f16x8 yl;
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+              yl[q] = (_Float16)zmix_lo(yw[q >> 1], -1.f, y[q]);
+              yl[q + 1] = (_Float16)zmix_hi(yw[q >> 1], -1.f, y[q + 1]);
+            }
+            *reinterpret_cast<f16x8*>(smem + ah) = yh;
+            *reinterpret_cast<f16x8*>(smem + ah + ZPART) = yl;
+            continue;
+          }
           if constexpr (SCVT) {
             // d = y - h exactly (Sterbenz), Xl8 = e4m3(d * ls), Xh8 = e4m3(h * hs) by the scaled
             // conversions (x / s: s = 1 / ls, 1 / hs, powers of two)
@@ -615,6 +647,8 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
   static_assert(KBZ % U == 0 && U % RA == 0 && (U / 2) % RG == 0 && RG > GD, "rings");
   f16x8 A16[RA][CT], B16[TW];
   i32x8 A8[RG][CT], B8[BPW];
+  f16x8 AL16[RA][CT], BL16[TW];   // W3: the Wl fragments and the step's Xl fragments
+  static_assert(!W3 || TAPA, "W3 runs the tap-major loop");
   const int n_ = n, p1_ = p1, ph0_ = ph0, pw0_ = pw0, ph1_ = ph1, pw1_ = pw1, g_ = g;
   const uint4* Wh = W.convz + (size_t)(CT * wc) * KBZ * 128 + lane;   // hi parts
   const uint4* W8 = W.conv8 + (size_t)(CT * wc) * GZ * 128 + lane;
@@ -638,6 +672,18 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
                     rs_h, vo_h, lo_h + (c_ * KBZ + kk_) * 2048, 0));                  \
       else                                                                            \
         S[c_] = __builtin_bit_cast(f16x8, Wh[((size_t)c_ * KBZ + kk_) * 128]);        \
+    }                                                                                 \
+  }
+  // W3: Wl (lo part) fragments of step KB: the hi part's + 1 KB
+#define Z_LOAD_AL16(S, KB)                                                            \
+  {                                                                                   \
+    const int kk_ = DIAG_L1 ? 0 : (KB) < KBZ ? (KB) : KBZ - 1;                        \
+    _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_) {                               \
+      if constexpr (WBUF)                                                             \
+        S[c_] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(       \
+                    rs_h, vo_h, lo_h + (c_ * KBZ + kk_) * 2048 + 1024, 0));           \
+      else                                                                            \
+        S[c_] = __builtin_bit_cast(f16x8, Wh[((size_t)c_ * KBZ + kk_) * 128 + 64]);   \
     }                                                                                 \
   }
   // e4m3 weight fragments of group GR (tap, chunk, term), channel tiles [C0, C0 + CT/2); with
@@ -708,11 +754,16 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
       sb_l[j] = 127 - (shj + 11), sb_h[j] = 127 - shj;
     }
 #pragma unroll
-    for (int p = 0; p < PD; ++p) Z_LOAD_A16(A16[p], p);
+    for (int p = 0; p < PD; ++p) {
+      Z_LOAD_A16(A16[p], p);
+      if constexpr (W3) Z_LOAD_AL16(AL16[p], p);
+    }
+    if constexpr (!W3) {
 #pragma unroll
-    for (int p = 0; p < GD; ++p) {
-      Z_LOAD_A8(A8[p], p, 0)
-      Z_LOAD_A8(A8[p], p, CT / 2)
+      for (int p = 0; p < GD; ++p) {
+        Z_LOAD_A8(A8[p], p, 0)
+        Z_LOAD_A8(A8[p], p, CT / 2)
+      }
     }
     if constexpr (TAPA) {
       static_assert(8 % RA == 0 && RG == 2 && !DIAG_NOLDS, "tap-major loop: 8 steps per iteration");
@@ -746,10 +797,57 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
     }                                                                                     \
   }
       Z_LOAD_B16T(B16, crow, coff, cm, 0);
+      // W3: the Xl fragments (part 1), same offsets as Z_LOAD_B16T
+#define Z_LOAD_BL16T(S16, ROW, OFF, M, CS)                                                 \
+  {                                                                                       \
+    const int o0_ = zsel(M[0], ROW[0] + g256 + 1024 * (CS), OFF[0]);                      \
+    const int o1_ = zsel(M[1], ROW[1] + g256 + 1024 * (CS), OFF[1]);                      \
+    _Pragma("unroll") for (int j_ = 0; j_ < BPW; ++j_) {                                  \
+      const char* base_ = smem + ZPART + bofs + j_ * ZBOARD;                              \
+      S16[2 * j_] = *reinterpret_cast<const f16x8*>(base_ + o0_);                         \
+      S16[2 * j_ + 1] = *reinterpret_cast<const f16x8*>(base_ + o1_);                     \
+    }                                                                                     \
+  }
 #pragma unroll 1
       for (int t = 0; t < 9; ++t) {
         int nrow[2], noff[2], nm[2];
         tap_addr(t < 8 ? t + 1 : 8, nrow, noff, nm);
+        if constexpr (W3) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int s = 8 * t + u;
+            // Wh*Xh and Wl*Xh on the step's Xh fragments; meanwhile its Xl fragments and the
+            // weight fragments PD steps ahead
+            __builtin_amdgcn_sched_barrier(0);
+            Z_LOAD_BL16T(BL16, crow, coff, cm, u);
+            Z_LOAD_A16(A16[(u + PD) % RA], s + PD);
+            Z_LOAD_AL16(AL16[(u + PD) % RA], s + PD);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+              for (int tt = 0; tt < TW; ++tt)
+                acc[ct * TW + tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A16[u % RA][ct], B16[tt], acc[ct * TW + tt], 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+              for (int tt = 0; tt < TW; ++tt)
+                acc[ct * TW + tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AL16[u % RA][ct], B16[tt], acc[ct * TW + tt], 0, 0, 0);
+            // Wh*Xl; meanwhile the next step's Xh fragments
+            __builtin_amdgcn_sched_barrier(0);
+            if (u < 7)
+              Z_LOAD_B16T(B16, crow, coff, cm, u + 1)
+            else
+              Z_LOAD_B16T(B16, nrow, noff, nm, 0)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+              for (int tt = 0; tt < TW; ++tt)
+                acc[ct * TW + tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A16[u % RA][ct], BL16[tt], acc[ct * TW + tt], 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i) crow[i] = nrow[i], coff[i] = noff[i], cm[i] = nm[i];
+          continue;
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int s = 8 * t + u;
@@ -800,6 +898,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
         for (int i = 0; i < 2; ++i) crow[i] = nrow[i], coff[i] = noff[i], cm[i] = nm[i];
       }
 #undef Z_LOAD_B16T
+#undef Z_LOAD_BL16T
     } else {
     Z_LOAD_B16(B16, 0);
     if constexpr (DIAG_NOLDS) Z_LOAD_B8(B8, 0);
@@ -879,12 +978,13 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
     stamp(st_epi);
   }
 #undef Z_LOAD_A16
+#undef Z_LOAD_AL16
 #undef Z_LOAD_A8
 #undef Z_LOAD_B16
 #undef Z_LOAD_B8
   if (overflow && !DIAG_L2 && !DIAG_L1 && !DIAG_NOB && !DIAG_NOLDS) atomicOr(D.pr.err, ERR_F16);
 
-  heads_reduce<NT, true, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
+  heads_reduce<NT, !W3, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
                          make_float4(__builtin_ldexpf(1.f, -(sh[0] + 11)), __builtin_ldexpf(1.f, -(sh[1] + 11)),
                                      __builtin_ldexpf(1.f, -(sh[2] + 11)), __builtin_ldexpf(1.f, -(sh[3] + 11))));
   stamp(st_heads);
@@ -911,6 +1011,7 @@ static void launch_z(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
   // the round-2 K loop (per-step addresses, global-address weights)
   if (var == 2097152) Z_LAUNCH(2097152, 512);
   else if (var == 8192) Z_LAUNCH(8192, 512);
+  else if (var == 268435456) Z_LAUNCH(268435456, 512);
   else if (var == 33554432) Z_LAUNCH(33554432, 512);
   else if (var == 8388608 + 16777216 + 33554432) Z_LAUNCH(8388608 + 16777216 + 33554432, 512);
   else if (var == 8388608 + 16777216) Z_LAUNCH(8388608 + 16777216, 512);
@@ -957,16 +1058,23 @@ void launch_net_z(const Dev& d, const NetWeights& w, const Pos* pos, const int32
   if (max_b <= 0) return;
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
   const int ncu = device_cus();
-  if (variant == 0 && ncu > 0) {   // the product: full rounds, then the tail launches (k_net_z above)
-    const dim3 blk(64 * ZCfg<0>::NW);
-    hipLaunchKernelGGL((k_net_z<false, 0, XB>), dim3((max_b + XB - 1) / XB), blk, 0, s, d, w, pos, count, max_b, mode,
+  // the product (and its f16x3 form W3): full rounds, then the tail launches (k_net_z above)
+  auto tailed = [&](auto var_t) {
+    constexpr int V = decltype(var_t)::value;
+    const dim3 blk(64 * ZCfg<V>::NW);
+    hipLaunchKernelGGL((k_net_z<false, V, XB>), dim3((max_b + XB - 1) / XB), blk, 0, s, d, w, pos, count, max_b, mode,
                        logits_out, values_out, nullptr, ncu);
-    hipLaunchKernelGGL((k_net_z<false, 0, 1>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
+    hipLaunchKernelGGL((k_net_z<false, V, 1>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, ncu);
-    hipLaunchKernelGGL((k_net_z<false, 0, 2>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
+    hipLaunchKernelGGL((k_net_z<false, V, 2>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, ncu);
-    hipLaunchKernelGGL((k_net_z<false, 0, 3>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
+    hipLaunchKernelGGL((k_net_z<false, V, 3>), dim3(ncu), blk, 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, ncu);
+  };
+  if (variant == 0 && ncu > 0) {
+    tailed(std::integral_constant<int, 0>{});
+  } else if (variant == 268435456 && ncu > 0) {
+    tailed(std::integral_constant<int, 268435456>{});
   } else {   // variant 1: the product kernel with 4 boards per workgroup throughout (the round-2 assignment)
     launch_z<false>(variant == 1 ? 0 : variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode,
                     logits_out, values_out, nullptr);
