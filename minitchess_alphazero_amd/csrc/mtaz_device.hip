@@ -953,6 +953,10 @@ __global__ __launch_bounds__(256, 1) void k_conv3x3(const float* __restrict__ in
   const float4* w0 = wpk + (size_t)(2 * wave) * 288 * 64 + lane;
   const float4* w1 = wpk + (size_t)(2 * wave + 1) * 288 * 64 + lane;
   f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  // Chunked accumulation: every tap's 256 k (32 groups) accumulates from zero and is then added
+  // into the master sums m** (round to nearest), so that each output takes 9 roundings at its full
+  // magnitude instead of one per MFMA (1152 two-product steps); as in k_net_y (mtaz_net16.hip, CH)
+  f32x16 m00 = {0}, m01 = {0}, m10 = {0}, m11 = {0};
   // Software pipeline over the 288 groups of 4 k-steps (k = tap*256 + ci): the weight
   // float4s of group s+2 and the 8 A values of group s+1 are issued before the 16 MFMAs
   // of group s; sched_barrier keeps the compiler from sinking them next to their use.
@@ -1004,7 +1008,12 @@ __global__ __launch_bounds__(256, 1) void k_conv3x3(const float* __restrict__ in
     acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[7], cb0.w, acc10, 0, 0, 0);
     acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[7], cb1.w, acc11, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+    if ((s4 & 31) == 31) {
+      m00 += acc00; m01 += acc01; m10 += acc10; m11 += acc11;
+      acc00 = (f32x16){0}; acc01 = (f32x16){0}; acc10 = (f32x16){0}; acc11 = (f32x16){0};
+    }
   }
+  acc00 = m00; acc01 = m01; acc10 = m10; acc11 = m11;   // (288 = 9 x 32: the last chunk is added)
   // epilogue: col = lane&31 -> channel; rows (r&3) + 8(r>>2) + 4*kh -> positions
 #pragma unroll
   for (int bb = 0; bb < 2; ++bb) {

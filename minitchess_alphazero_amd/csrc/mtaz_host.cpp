@@ -1224,7 +1224,8 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
 
 static void launch_network(mtaz_engine* h, const Pos* pos, const int32_t* count, int max_b, int mode, float* logits,
                            float* values, hipEvent_t eb, hipEvent_t ee) {
-  // f16x3 variant 268435456: k_net_y's arithmetic in k_net_z's structure (mtaz_net8.hip, W3)
+  // f16x3 variant 268435456 (diagnostic library): k_net_y's arithmetic in k_net_z's structure
+  // (mtaz_net8.hip, W3; without k_net_y's chunked accumulation)
   if (h->precision == NET_F16F8 || (h->precision == NET_F16X3 && h->variant == 268435456)) {
     launch_net_z(h->d, h->w, pos, count, max_b, mode, logits, values, h->stream, eb, ee, h->variant);
   } else if (h->precision == NET_F16X3) {
@@ -1299,7 +1300,7 @@ extern "C" int mtaz_diag_select_stamps(unsigned long long* out8, int reset) {
 
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
-  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 1024 || variant == 268435456;
+  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 1024;
   if (h->precision == NET_F16F8)
     ok = ok || variant == 1 || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 ||
          variant == 33554432 || variant == 8388608 + 16777216 + 33554432;

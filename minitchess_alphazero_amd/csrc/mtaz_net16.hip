@@ -58,7 +58,8 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
 #define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
 
 // VAR: 0 = product; 1024 = the epilogue in unfused form (bit-identity reference for the
-// product's v_fma_mix epilogue, test_gpu_net.py).  Round 1's schedule A/B variants (whole-k-block
+// product's v_fma_mix epilogue, test_gpu_net.py); 4096 (diagnostic library) = one accumulation
+// chain per layer (round 2's k_net_y, see CH below).  Round 1's schedule A/B variants (whole-k-block
 // steps, sched_group_barrier interleaves, 8 waves of 32 channels) measured within 1% of the
 // pinned half-steps and were retired.
 // NVB / ncu: the tail-balanced board assignment of k_net_z (mtaz_net8.hip): with ncu > 0 the
@@ -107,17 +108,25 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // the lane's output squares: n (tile 0) and p1 = 16 + n (tile 1; 30, 31 are padding)
   const int p1 = 16 + n;
   const int ph0 = n / 5, pw0 = n % 5, ph1 = p1 / 5, pw1 = p1 % 5;
-  // VAR 4096 (CH): chunked accumulation.  The MFMAs of every U = 12 k-blocks accumulate from zero
-  // into acc, which is then added into the master sums mst (fp32, round to nearest; the next
-  // chunk's first MFMAs start from C = 0).  Each output takes 6 roundings at its full magnitude per
-  // layer instead of one per MFMA (216), and the residual (seeded into mst) no longer sits under
-  // every MFMA's rounding.  The epilogue reads mst + acc.
-  constexpr bool CH = (VAR & 4096) != 0;
-  f32x4v acc[CT * 8], mst[CH ? CT * 8 : 1];
+  // Chunked accumulation (CH; VAR 4096 = round 2's single chain, for A/B only).  The MFMAs of
+  // every U = 12 k-blocks (a chunk) accumulate from zero into acc, and each tile's chunk sum is
+  // added into the master sums mst (fp32, round to nearest).  Each output then takes 6 roundings at
+  // its full magnitude per layer instead of one per MFMA (216: a 16x16x32 f16 MFMA rounds C + its
+  // 32 products once), and the residual (seeded into mst) no longer sits under every MFMA's
+  // rounding.  On the stress net (trunk activations ~3300) this takes the priors' error from
+  // 1.5e-5 to 2.7e-6 of an fp64 forward (tools/stress_error.py, tools/dump_net.py) for +3% time.
+  // The adds are staggered so that they issue between MFMAs on other tiles: the square-tile-0
+  // tiles' during the chunk's last half-step (square tile 1), the square-tile-1 tiles' during the
+  // next chunk's first half-step (square tile 0), whose MFMAs start from C = 0.  After a layer's
+  // K loop the square-tile-1 tiles are still pending: the epilogue reads mst (+ acc for those).
+  // (Measured and dropped: chunks of 6 k-blocks, 1.2e-6 for +7.4%; the residual alone kept out of
+  // the chain, 9.7e-6 for +7.5%.)
+  constexpr bool CH = (VAR & 4096) == 0, MS = CH;
+  f32x4v acc[CT * 8], mst[MS ? CT * 8 : 1];
 #pragma unroll
   for (int i = 0; i < CT * 8; ++i) acc[i] = (f32x4v){0};
 #pragma unroll
-  for (int i = 0; i < (CH ? CT * 8 : 1); ++i) mst[i] = (f32x4v){0};
+  for (int i = 0; i < (MS ? CT * 8 : 1); ++i) mst[i] = (f32x4v){0};
   int overflow = 0;
 
   // Dynamic range.  The image holds x * 2^-xs in f16 hi/lo with one exponent xs per workgroup
@@ -161,10 +170,12 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       for (int t = 0; t < 2 * NVB; ++t) {
         const int bb = t >> 1, pt = t & 1;
         f32x4v& acc_t = acc[ct * 8 + t];
-        f32x4v& a = CH ? mst[CH ? ct * 8 + t : 0] : acc_t;   // the sum; the next layer's seed goes here
+        f32x4v& a = MS ? mst[MS ? ct * 8 + t : 0] : acc_t;   // the sum; the next layer's seed goes here
         if constexpr (CH) {
-          a += acc_t;
-          acc_t = (f32x4v){0};
+          if (pt == 1) {   // pending (square tile 1); zeroed for the next layer's first add
+            a += acc_t;
+            acc_t = (f32x4v){0};
+          }
         }
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
@@ -253,6 +264,10 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       YMMA3(SA, SB);
     }
   }
+  if constexpr (CH) {   // the stem's square-tile-0 sums (the epilogue adds the square-tile-1 ones)
+#pragma unroll
+    for (int i = 0; i < CT * 8; i += 2) mst[CH ? i : 0] += acc[i];
+  }
   epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f,
            __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mx_img, W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f);
   stamp(st_stem);
@@ -289,7 +304,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   }
 // product half-step: 12 chunks of 4 MFMAs in fixed program order (sched_barrier between
 // chunks), LDS reads 2 per chunk in chunks 0-3, weight loads 1 per chunk in chunks 4-7
-#define HALF_PINNED(KB, PT, AC, AP, BC, BN, KBN, PTN)                                 \
+#define HALF_PINNED(KB, PT, AC, AP, BC, BN, KBN, PTN, FIRST, ADDT)                    \
   {                                                                                   \
     const int kk_ = (KBN) < KBY ? (KBN) : KBY - 1;                                    \
     const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
@@ -314,13 +329,27 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
             const int ct_ = (CT / 2) * (PT) + (q_ >> 1), pp_ = q_ & 1;                \
             AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
           }                                                                           \
+        /* CH: the chunk sums of square tile ADDT into mst, 1-2 tiles per chunk */      \
+        /* (tile j = 4 ct + board goes with chunk floor(3j / 4)) */                    \
+        if (CH && (ADDT) >= 0) {                                                      \
+          const int ja_ = (4 * c_ + 2) / 3, jb_ = ja_ + 1;                            \
+          if ((ja_ & 3) < NVB) {                                                      \
+            const int ix_ = (ja_ >> 2) * 8 + (ja_ & 3) * 2 + ((ADDT) > 0);            \
+            mst[CH ? ix_ : 0] += acc[ix_];                                            \
+          }                                                                           \
+          if (jb_ < 16 && (3 * jb_) / 4 == c_ && (jb_ & 3) < NVB) {                   \
+            const int ix_ = (jb_ >> 2) * 8 + (jb_ & 3) * 2 + ((ADDT) > 0);            \
+            mst[CH ? ix_ : 0] += acc[ix_];                                            \
+          }                                                                           \
+        }                                                                             \
         __builtin_amdgcn_sched_barrier(0);                                            \
       }                                                                               \
       const int ps_ = i_ / (4 * CT), ct_ = (i_ >> 2) % CT, bb_ = i_ & 3;              \
       const int wp_ = ps_ == 2 ? 1 : 0, xp_ = ps_ == 1 ? 1 : 0;                       \
       if (bb_ < NVB)                                                                  \
         acc[ct_ * 8 + bb_ * 2 + (PT)] = __builtin_amdgcn_mfma_f32_16x16x32_f16(       \
-            AC[2 * ct_ + wp_], BC[xp_ * 4 + bb_], acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0); \
+            AC[2 * ct_ + wp_], BC[xp_ * 4 + bb_],                                     \
+            (CH && (FIRST) && ps_ == 0) ? (f32x4v){0} : acc[ct_ * 8 + bb_ * 2 + (PT)], 0, 0, 0); \
     }                                                                                 \
     __builtin_amdgcn_sched_barrier(0);                                                \
   }
@@ -331,15 +360,9 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     for (int kb = 0; kb < KBY; kb += U) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        HALF_PINNED(kb + u, 0, A[u % RS], A[(u + PD) % RS], BH[0], BH[1], kb + u, 1);
-        HALF_PINNED(kb + u, 1, A[u % RS], A[(u + PD) % RS], BH[1], BH[0], kb + u + 1, 0);
-      }
-      if constexpr (CH) {   // the chunk into the master sums; the next chunk starts from C = 0
-#pragma unroll
-        for (int i = 0; i < CT * 8; ++i) {
-          mst[CH ? i : 0] += acc[i];
-          acc[i] = (f32x4v){0};
-        }
+        HALF_PINNED(kb + u, 0, A[u % RS], A[(u + PD) % RS], BH[0], BH[1], kb + u, 1, u == 0, u == 0 ? 1 : -1);
+        HALF_PINNED(kb + u, 1, A[u % RS], A[(u + PD) % RS], BH[1], BH[0], kb + u + 1, 0, u == 0,
+                    u == U - 1 ? 0 : -1);
       }
     }
     stamp(st_k);
@@ -385,6 +408,7 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
     hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == 4096)
     hipLaunchKernelGGL((k_net_y<S, 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+
   else
     hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
 }

@@ -25,8 +25,7 @@ def _softmax(x):
 
 # every build the product library accepts (mtaz_set_net_variant): f16f8 = k_net_z (default),
 # f16f6 = k_net_z with e2m3 cross terms, f16x3 = k_net_y, fp32 = the fp32 MFMA path
-NET_KERNELS = {'f16f8': ('f16f8', 0), 'f16f6': ('f16f8', 8192), 'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0),
-               'f16x3w': ('f16x3', 268435456)}
+NET_KERNELS = {'f16f8': ('f16f8', 0), 'f16f6': ('f16f8', 8192), 'f16x3': ('f16x3', 0), 'fp32': ('fp32', 0)}
 
 
 @pytest.fixture(scope='module', params=list(NET_KERNELS))
@@ -118,7 +117,7 @@ def test_product_library_rejects_untested_variants():
     eng = Engine(n_games=4, sims=2)
     for prec, good, bad in (('f16f8', [0, 1, 8192, 2097152, 25165824, 33554432, 58720256],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
-                            ('f16x3', [0, 1, 1024], [512, 4, 8, 2048, 8192])):
+                            ('f16x3', [0, 1, 1024], [512, 4, 8, 2048, 8192, 4096, 268435456])):
         eng.set_precision(prec)
         for v in good:
             eng.set_net_variant(v)

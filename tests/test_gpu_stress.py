@@ -6,7 +6,12 @@ the build container), with one 64-sim reference self-play game.
 
   * network parity, the north_star bound for every product precision that claims it: priors
     (softmax over the legal list) and values within 1e-5, logits within 1e-5 of each row's
-    largest |logit| (the fp32 error scale at these magnitudes);
+    largest |logit| (the fp32 error scale at these magnitudes).  Both kernels accumulate each
+    layer in chunks added into fp32 master sums (k_net_y: 12 k-blocks; the fp32 path: one tap):
+    with one accumulation chain per layer (round 2) the MFMA roundings at the outputs' full
+    magnitude took k_net_y to 1.4e-5 on the priors and the fp32 path to 2.5e-5 on the logits
+    (tools/stress_error.py, tools/dump_net.py: the torch fp32 reference is itself 1.3e-6 from an
+    fp64 forward on these positions);
   * the priors and values the search consumes (device-written leaf results), same bound;
   * L1: the reference's 64-sim game bit-exact with host leaves (batch-1 torch CPU);
   * L3: the GPU network end to end, divergences only at near-ties the measured leaf deviations
