@@ -179,8 +179,9 @@ def main():
     ap.add_argument('--default-sims', type=int, default=36,
                     help="one more timed step at the repo's default sims per move (app/base.py:25: 36; 0 = skip), "
                          'reported with its CPU baseline as at_repo_default_sims')
-    ap.add_argument('--memo', type=int, default=1, choices=[0, 1, 2],
-                    help='leaf memo: 1 = per game (default), 2 = per game + batch, 0 = evaluate every leaf')
+    ap.add_argument('--memo', type=int, default=2, choices=[0, 1, 2],
+                    help='leaf memo: 2 = per game + batch (default), 1 = per game, 0 = evaluate every leaf '
+                         '(results identical in every mode)')
     ap.add_argument('--traffic-json', default=os.path.join(HERE, 'profiles', 'conv_traffic.json'))
     ap.add_argument('--weights', default='', help='state_dict file (safetensors or torch.save) instead of random '
                                                   'init (BASELINE config 3: tests/golden/c3/c3.safetensors)')

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Summarise the `pmc` step of tools/gpu.sh (gpurun_out/OUT/pmc) into profiles/conv_traffic.json.
 
-Per network-kernel dispatch: HBM-side bytes = 2 x FETCH_SIZE (gfx950 tallies a 16-B/lane streaming
+Per network evaluation (one launch group: the 4-boards-per-workgroup kernel and its three tail
+launches, k_net_[yz]<., ., 1..3>, which mostly exit at once; the sums over every dispatch divided
+by the number of main launches): HBM-side bytes = 2 x FETCH_SIZE (gfx950 tallies a 16-B/lane streaming
 read at half its bytes, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both reported in KB.
 FETCH_SIZE also counts Infinity-Cache hits, so this is fabric-side traffic (an upper bound
 on HBM bytes).  The L2 hit rate is TCC_HIT / (TCC_HIT + TCC_MISS).
@@ -17,11 +19,14 @@ from collections import defaultdict
 
 
 KERNELS = set()
+MAIN = re.compile(r'k_net_[yz]<false, \d+, 4>')
 
 
 def read_counters(root):
-    """{counter: [per-dispatch value]} over every counter_collection CSV under root."""
+    """{counter: (sum over every network dispatch, number of main launches)} over every
+    counter_collection CSV under root (one pass per counter group)."""
     vals = defaultdict(dict)
+    mains = defaultdict(set)
     for path in glob.glob(os.path.join(root, '**', '*counter_collection.csv'), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
@@ -31,12 +36,15 @@ def read_counters(root):
                 key = (path, row['Dispatch_Id'])
                 name = row['Counter_Name']
                 vals[name][key] = vals[name].get(key, 0.0) + float(row['Counter_Value'])
-    return {k: list(v.values()) for k, v in vals.items()}
+                if MAIN.search(row['Kernel_Name']):
+                    mains[name].add(key)
+    return {k: (sum(v.values()), len(mains[k]), len(v)) for k, v in vals.items()}
 
 
 def bench_config(root):
     """games / sims of the profiled bench run, from the JSON line in a pass log."""
-    for log in sorted(glob.glob(os.path.join(root, 'p*.log'))):
+    logs = glob.glob(os.path.join(root, 'p*.log')) + glob.glob(os.path.join(os.path.dirname(root.rstrip('/')), 'pmc_p*.log'))
+    for log in sorted(logs):
         for line in open(log):
             if line.startswith('{') and '"metric"' in line:
                 d = json.loads(line)
@@ -51,7 +59,7 @@ def main():
                                                   'profiles', 'conv_traffic.json'))
     args = ap.parse_args()
     c = read_counters(args.root)
-    mean = lambda k: sum(c[k]) / len(c[k]) if c.get(k) else None
+    mean = lambda k: c[k][0] / c[k][1] if c.get(k) and c[k][1] else None   # per evaluation
     fetch_kb, write_kb = mean('FETCH_SIZE'), mean('WRITE_SIZE')
     hit, miss = mean('TCC_HIT_sum'), mean('TCC_MISS_sum')
     mfma, grbm = mean('SQ_VALU_MFMA_BUSY_CYCLES'), mean('GRBM_GUI_ACTIVE')
@@ -62,7 +70,8 @@ def main():
     out = {
         'kernel': '+'.join(sorted(KERNELS)),
         'games': games, 'sims': sims,
-        'dispatches': {k: len(v) for k, v in c.items()},
+        'dispatches': {k: v[2] for k, v in c.items()},
+        'evaluations': {k: v[1] for k, v in c.items()},
         'fetch_size_kb_per_launch': fetch_kb,
         'write_size_kb_per_launch': write_kb,
         'hbm_bytes_per_launch': (2 * fetch_kb + write_kb) * 1024 if fetch_kb is not None and write_kb is not None else None,
@@ -73,7 +82,8 @@ def main():
         'sq_wave_cycle_shares': ({'active_inst_any': active / wave, 'wait_inst_any': wait_inst / wave,
                                   'wait_any': wait_any / wave} if wave else None),
         'lds_bank_conflict_frac': conf / ldsact if conf is not None and ldsact else None,
-        'method': 'rocprofv3 --pmc, one pass per counter group, --kernel-include-regex k_net_[yz]; '
+        'method': 'rocprofv3 --pmc, one pass per counter group, --kernel-include-regex k_net_[yz]; per evaluation = '
+                  'sums over the main launch and its tail launches / main launches; '
                   'bytes = (2*FETCH_SIZE + WRITE_SIZE) KB * 1024 (gfx950 FETCH_SIZE half-count correction); '
                   'mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs)',
     }
