@@ -728,7 +728,11 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
   if (lane == 0) T.node_hdr[nbase + n].tval = D.lf.v[i];   // kept for the leaf memo (Params::memo)
   if (D.pr.memo >= 2 && D.bm.cap && k <= MEMO_K) {
     // batch memo insert: claim a slot (0 -> 1), write, publish (-> 2); a slot another leaf of this
-    // launch claimed is passed over (at worst a position is kept twice, with identical results)
+    // launch claimed is passed over (at worst a position is kept twice, with identical results).
+    // Readers (k_select) run in later launches on the same stream, so the kernel boundary orders
+    // the entry's writes before any lookup: no fence, and the publish is a plain store.  Within
+    // this launch a prober may see state 2 before the key: it then passes over the slot or, on a
+    // stale key equal to its own, skips the insert (a memo miss later, never a wrong entry).
     const BatchMemo& B = D.bm;
     const Pos p = D.lf.pos[i];
     uint32_t slot = NONE;
@@ -754,8 +758,7 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
         B.key[slot] = p;
         B.v[slot] = D.lf.v[i];
         B.k[slot] = (uint16_t)k;
-        __threadfence();
-        atomicExch(&B.state[slot], 2u);
+        B.state[slot] = 2u;
       }
     }
   }

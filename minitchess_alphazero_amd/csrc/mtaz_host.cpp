@@ -1341,14 +1341,16 @@ extern "C" int mtaz_set_weights_slot(mtaz_engine* h, int slot, const float* cons
 // agents search with the same network
 static void sync_memo(mtaz_engine* h) { h->d.pr.memo = h->agent_slot[0] == h->agent_slot[1] ? h->memo : 0; }
 
-// The batch memo's table: 2 slots per possible evaluation of a play (2 G tables x move_cap searches x
-// sims), a power of two, at most 2^28 slots (222 B each).
+// The batch memo's table.  A play evaluates at most one leaf per game and simulation; the table
+// holds 2 slots per leaf of a 64-ply game (move_cap searches per agent, at most 32 each), a power
+// of two, at most 2^26 slots (222 B each): 2^25 = 7.4 GB for 4096 games x 64 sims.  A full table,
+// or a probe run past MEMO_PROBES, only skips inserts (memo misses, never a wrong entry).
 static int ensure_batch_memo(mtaz_engine* h) {
   if (h->memo < 2 || h->d.bm.cap) return 0;
-  const int max_moves = h->move_cap > 0 ? h->move_cap : 200;
-  const uint64_t want = 2ull * 2 * (uint64_t)h->G * (uint64_t)max_moves * (uint64_t)h->sims;
+  const int plies = 2 * (h->move_cap > 0 && h->move_cap < 32 ? h->move_cap : 32);
+  const uint64_t want = 2ull * (uint64_t)h->G * (uint64_t)plies * (uint64_t)h->sims;
   uint64_t cap = 1024;
-  while (cap < want && cap < (1ull << 28)) cap <<= 1;
+  while (cap < want && cap < (1ull << 26)) cap <<= 1;
   BatchMemo& B = h->d.bm;
   auto grab = [&](auto** p, size_t elt) -> int {
     void* q = nullptr;
