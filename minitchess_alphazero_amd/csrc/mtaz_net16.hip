@@ -72,8 +72,9 @@ __device__ __forceinline__ void add4(f32x4v& m, const f32x4v& a) {
 #define YMMA3(SA, SB) YMMA(SA, SB, 0, 0) YMMA(SA, SB, 0, 1) YMMA(SA, SB, 1, 0)
 
 // VAR: 0 = product; 1024 = the epilogue in unfused form (bit-identity reference for the
-// product's v_fma_mix epilogue, test_gpu_net.py); 4096 (diagnostic library) = one accumulation
-// chain per layer (round 2's k_net_y, see CH below).  Round 1's schedule A/B variants (whole-k-block
+// product's v_fma_mix epilogue, test_gpu_net.py); 114688 = the K loop without the offset table,
+// the buffer loads and the 2-slot weight ring (bitwise equal, test_y_loop_forms_bit_identical);
+// 4096 (diagnostic library) = one accumulation chain per layer (round 2's k_net_y, see CH below).  Round 1's schedule A/B variants (whole-k-block
 // steps, sched_group_barrier interleaves, 8 waves of 32 channels) measured within 1% of the
 // pinned half-steps and were retired.
 // NVB / ncu: the tail-balanced board assignment of k_net_z (mtaz_net8.hip): with ncu > 0 the
@@ -87,7 +88,12 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
                                                   float* __restrict__ logits_out, float* __restrict__ values_out,
                                                   unsigned long long* __restrict__ stamps, int ncu) {
   static_assert(NVB >= 1 && NVB <= XB, "boards per workgroup");
-  __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB];
+  // OT (product; VAR 32768 = off): the K loop's fragment offsets come from a per-lane LDS table of
+  // the source rows [tap 9][square tile 2][lane 64] (one ds_read_b32 per half-step, issued a
+  // half-step ahead) instead of recomputing src_row (~20 VALU / SALU per half-step)
+  constexpr bool OT = (VAR & 32768) == 0;
+  constexpr int OTB = OT ? 9 * 2 * 64 * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB + OTB];
   int b0, nb;
   {
     const int n = count ? *count : max_b;
@@ -255,6 +261,16 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // ---------------- stem: conv3x3 8->256, K = 3 k-blocks of (4 taps x 8 channels) ----------
   char* simg = smem + IMGB;
   stem_input<NT>(smem, simg, pos, b0, nb, W, tid);
+  if constexpr (OT) {   // entry: row * RB | (g ^ (row & 15)) for square n (tile 0) or 16 + n (tile 1)
+    if (wave == 0) {
+      int* ot = reinterpret_cast<int*>(smem + IMGB + AUXB);
+      for (int e = 0; e < 18; ++e) {
+        const int tap = e >> 1, pt = e & 1;
+        const int r = pt ? src_row(p1, ph1, pw1, tap) : src_row(n, ph0, pw0, tap);
+        ot[e * 64 + lane] = r * RB | (g ^ (r & 15));
+      }
+    }
+  }
   __syncthreads();
   {
     const uint4* Ws = W.stemy + (size_t)(CT * wave) * 3 * 128 + lane;
@@ -292,17 +308,34 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // activation fragments of one tile are live (a 2 x 8-fragment ring): the next half's are read
   // from LDS during the current half, in 12 chunks of 4 MFMAs whose order sched_barrier pins
   // (HALF_PINNED: no accumulator copies, no spills).
-  constexpr int PD = 2, RS = 3, U = CH ? 12 : 6;
+  // the weight ring: 2 slots, one k-block ahead (VAR 16384: 3 slots, two ahead, round 2's)
+  constexpr int PD = (VAR & 16384) ? 2 : 1, RS = PD + 1, U = CH ? 12 : 6;
+  const char* otab = smem + IMGB + AUXB + 4 * lane;   // OT: this lane's column of the table
+  int tpre = 0;                                        // OT: the next half-step's table entry
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
   f16x8 A[RS][2 * CT], BH[2][8];
   const uint4* Wl = W.convy + (size_t)(CT * wave) * KBY * 128 + lane;
+  // WB (product; VAR 65536 = off): weight fragments by buffer loads (descriptor over convy, the
+  // wave's lane offset in a VGPR, layer / k-block / tile offsets in an SGPR) instead of 64-bit
+  // global addresses
+  constexpr bool WB = (VAR & 65536) == 0;
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)W.convy, (short)0, 0x7ffffff0, 0x00020000);
+  const int voy = ((CT * wave) * KBY * 128 + lane) * 16;
+  int lofs = 0;   // WB: the layer's byte offset in convy
 #define LOAD_A(S, KB)                                                                 \
   {                                                                                   \
     const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
     const uint4* p_ = Wl + (size_t)kk_ * 128;                                         \
     _Pragma("unroll") for (int c_ = 0; c_ < CT; ++c_) {                               \
-      S[2 * c_] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128]);                      \
-      S[2 * c_ + 1] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128 + 64]);             \
+      if constexpr (WB) {                                                             \
+        S[2 * c_] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(   \
+            rsy, voy, lofs + (c_ * KBY + kk_) * 2048, 0));                            \
+        S[2 * c_ + 1] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128( \
+            rsy, voy, lofs + (c_ * KBY + kk_) * 2048 + 1024, 0));                     \
+      } else {                                                                        \
+        S[2 * c_] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128]);                    \
+        S[2 * c_ + 1] = __builtin_bit_cast(f16x8, p_[c_ * KBY * 128 + 64]);           \
+      }                                                                               \
     }                                                                                 \
   }
 // one square tile's fragments of k-block KB: S[part*4 + board]
@@ -321,9 +354,18 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
 #define HALF_PINNED(KB, PT, AC, AP, BC, BN, KBN, PTN, FIRST, ADDT)                    \
   {                                                                                   \
     const int kk_ = (KBN) < KBY ? (KBN) : KBY - 1;                                    \
-    const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
-    const int r_ = (PTN) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);  \
-    const int o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                \
+    int o_;                                                                           \
+    if constexpr (OT) {                                                               \
+      /* tpre holds the entry of (KBN, PTN); load the one of (KB + 1, PT) for the next half */ \
+      const int t_ = tpre, x_ = t_ ^ (4 * (kk_ & 7));                                 \
+      o_ = (t_ & ~31) | ((x_ & 31) << 4);                                             \
+      const int kq_ = ((KB) + 1) < KBY ? ((KB) + 1) : KBY - 1;                        \
+      tpre = *reinterpret_cast<const int*>(otab + ((kq_ >> 3) * 2 + (PT)) * 256);     \
+    } else {                                                                          \
+      const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                             \
+      const int r_ = (PTN) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);\
+      o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                        \
+    }                                                                                 \
     const int ka_ = ((KB) + PD) < KBY ? ((KB) + PD) : KBY - 1;                        \
     const uint4* pa_ = Wl + (size_t)ka_ * 128;                                        \
     _Pragma("unroll") for (int i_ = 0; i_ < 12 * CT; ++i_) {                          \
@@ -341,7 +383,11 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         _Pragma("unroll") for (int q_ = 0; q_ < CT; ++q_)                             \
           if (q_ >= g0_ && q_ < g1_) {                                                \
             const int ct_ = (CT / 2) * (PT) + (q_ >> 1), pp_ = q_ & 1;                \
-            AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
+            if constexpr (WB)                                                         \
+              AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128( \
+                  rsy, voy, lofs + (ct_ * KBY + ka_) * 2048 + pp_ * 1024, 0));        \
+            else                                                                      \
+              AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, pa_[ct_ * KBY * 128 + pp_ * 64]); \
           }                                                                           \
         /* CH: the chunk sums of square tile ADDT into mst, 1-2 tiles per chunk */      \
         /* (tile j = 4 ct + board goes with chunk floor(3j / 4)) */                    \
@@ -371,6 +417,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
 #pragma unroll
     for (int p = 0; p < PD; ++p) LOAD_A(A[p], p);
     LOAD_BH(BH[0], 0, 0);
+    if constexpr (OT) tpre = *reinterpret_cast<const int*>(otab + 1 * 256);   // (k-block 0, tile 1)
     for (int kb = 0; kb < KBY; kb += U) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -381,6 +428,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     }
     stamp(st_k);
     Wl += CONVX_U4_PER_LAYER;
+    lofs += (int)(CONVX_U4_PER_LAYER * 16);
     __syncthreads();   // every wave has finished reading this layer's input image
     // output bound (the margin 1 + 2^-10 covers the rounding of the bound's own arithmetic)
     if ((L & 1) == 0) {
@@ -420,6 +468,8 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
                      unsigned long long* stamps) {
   if (var == 1024)
     hipLaunchKernelGGL((k_net_y<S, 1024>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == 114688)   // the K loop before the offset table, buffer loads and 2-slot ring
+    hipLaunchKernelGGL((k_net_y<S, 114688>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == 4096)
     hipLaunchKernelGGL((k_net_y<S, 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
 

@@ -104,7 +104,9 @@ class Engine:
 
     def set_net_variant(self, variant):
         """Select a parity-tested build of the current precision's network kernel (0 = product;
-        set_precision resets it).  f16x3 (k_net_y): 1024 = the epilogue in unfused form.  f16f8
+        set_precision resets it).  f16x3 (k_net_y): 1 = 4 boards per workgroup in every round (no
+        tail launches), 1024 = the epilogue in unfused form, 114688 = the K loop without the LDS
+        offset table, buffer loads and 2-slot weight ring; all bitwise equal to 0.  f16f8
         (k_net_z): 1 = 4 boards per workgroup in every round (no tail launches), 2097152 = the
         epilogue in unfused form, 8192 = e2m3 (fp6) cross terms,
         25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),

@@ -117,7 +117,7 @@ def test_product_library_rejects_untested_variants():
     eng = Engine(n_games=4, sims=2)
     for prec, good, bad in (('f16f8', [0, 1, 8192, 2097152, 25165824, 33554432, 58720256],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
-                            ('f16x3', [0, 1, 1024], [512, 4, 8, 2048, 8192, 4096, 268435456])):
+                            ('f16x3', [0, 1, 1024, 114688], [512, 4, 8, 2048, 8192, 4096, 268435456, 16384, 32768])):
         eng.set_precision(prec)
         for v in good:
             eng.set_net_variant(v)
@@ -171,6 +171,31 @@ def test_z_loop_forms_bit_identical():
         eng.set_net_variant(0)
         l0, v0 = eng.evaluate(pos)
         eng.set_net_variant(25165824)
+        l1, v1 = eng.evaluate(pos)
+        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
+def test_y_loop_forms_bit_identical():
+    """k_net_y's K loop with the LDS offset table, buffer-loaded weights and the 2-slot weight ring
+    (the product) computes exactly the loop before them (variant 114688): logits and values bitwise
+    equal on an ordinary, a wide-range and a tiny-activation net.  1024 boards = one full round of
+    4 boards per workgroup on 256 CUs, so both builds group the boards alike (variant 114688 has no
+    tail launches)."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from minitchess_alphazero_amd.network import Network
+    from tests_positions import random_fens
+    import torch
+    torch.manual_seed(0)
+    pos = np.stack([pos_from_fen(f) for f in random_fens(1024, seed=17)])
+    for net in (Network(), _wide_range_net(), _tiny_activation_net()):
+        eng = Engine(n_games=1024, sims=4)
+        eng.set_precision('f16x3')
+        eng.set_weights(net)
+        eng.set_net_variant(0)
+        l0, v0 = eng.evaluate(pos)
+        eng.set_net_variant(114688)
         l1, v1 = eng.evaluate(pos)
         assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
         assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
