@@ -366,6 +366,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       const int r_ = (PTN) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);\
       o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                        \
     }                                                                                 \
+    const int o1_ = o_ + PARTB;                                                       \
     const int ka_ = ((KB) + PD) < KBY ? ((KB) + PD) : KBY - 1;                        \
     const uint4* pa_ = Wl + (size_t)ka_ * 128;                                        \
     _Pragma("unroll") for (int i_ = 0; i_ < 12 * CT; ++i_) {                          \
@@ -377,9 +378,10 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         const int l0_ = c_ < 4 ? 2 * c_ : 0, l1_ = c_ < 4 ? 2 * c_ + 2 : 0;           \
         const int g0_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 4 : 0;                        \
         const int g1_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 3 : 0;                        \
+        /* part 1 from its own base (o_ + PARTB): the board offsets stay 16-bit immediates */ \
         _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_)                              \
           if (q_ >= l0_ && q_ < l1_ && (q_ & 3) < NVB)                                \
-            BN[q_] = *reinterpret_cast<const f16x8*>(smem + (q_ >> 2) * PARTB + (q_ & 3) * IROWS * RB + o_); \
+            BN[q_] = *reinterpret_cast<const f16x8*>(smem + ((q_ >> 2) ? o1_ : o_) + (q_ & 3) * IROWS * RB); \
         _Pragma("unroll") for (int q_ = 0; q_ < CT; ++q_)                             \
           if (q_ >= g0_ && q_ < g1_) {                                                \
             const int ct_ = (CT / 2) * (PT) + (q_ >> 1), pp_ = q_ & 1;                \
