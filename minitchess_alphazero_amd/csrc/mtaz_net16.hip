@@ -319,6 +319,14 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // wave's lane offset in a VGPR, layer / k-block / tile offsets in an SGPR) instead of 64-bit
   // global addresses
   constexpr bool WB = (VAR & 65536) == 0;
+  // timing-only diagnostic forms (diagnostic library; wrong results by construction): the K loop
+  // without its weight loads (DX_NOW, 1 << 20), without its fragment LDS reads (DX_NOB, 1 << 21),
+  // without the chunk adds into the master sums (DX_NOADD, 1 << 22)
+  // EL (1 << 23): every weight load of the next k-block issued in the first half-step of the
+  // current one (the ring slot is free from its start), so a load has ~1.5 k-blocks of latency
+  // instead of ~0.4 for the second half's loads; the same values, so bitwise the same results
+  constexpr bool EL = (VAR & (1 << 23)) != 0;
+  constexpr bool DX_NOW = (VAR & (1 << 20)) != 0, DX_NOB = (VAR & (1 << 21)) != 0, DX_NOADD = (VAR & (1 << 22)) != 0;
   const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)W.convy, (short)0, 0x7ffffff0, 0x00020000);
   const int voy = ((CT * wave) * KBY * 128 + lane) * 16;
   int lofs = 0;   // WB: the layer's byte offset in convy
@@ -376,15 +384,18 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         /* chunk c_ issues LDS reads [l0_, l1_) and weight loads [g0_, g1_) of the next half */ \
         /* 2 LDS reads per chunk 0-3, 1 load per chunk 4-7 */                        \
         const int l0_ = c_ < 4 ? 2 * c_ : 0, l1_ = c_ < 4 ? 2 * c_ + 2 : 0;           \
-        const int g0_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 4 : 0;                        \
-        const int g1_ = (c_ >= 4 && c_ < 4 + CT) ? c_ - 3 : 0;                        \
+        /* EL: all 2 CT loads of the next k-block in the first half-step, chunks 1..2CT */ \
+        const int g0_ = EL ? (((PT) == 0 && c_ >= 1 && c_ <= 2 * CT) ? c_ - 1 : 0)     \
+                           : ((c_ >= 4 && c_ < 4 + CT) ? c_ - 4 : 0);                 \
+        const int g1_ = EL ? (((PT) == 0 && c_ >= 1 && c_ <= 2 * CT) ? c_ : 0)         \
+                           : ((c_ >= 4 && c_ < 4 + CT) ? c_ - 3 : 0);                 \
         /* part 1 from its own base (o_ + PARTB): the board offsets stay 16-bit immediates */ \
         _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_)                              \
-          if (q_ >= l0_ && q_ < l1_ && (q_ & 3) < NVB)                                \
+          if (!DX_NOB && q_ >= l0_ && q_ < l1_ && (q_ & 3) < NVB)                     \
             BN[q_] = *reinterpret_cast<const f16x8*>(smem + ((q_ >> 2) ? o1_ : o_) + (q_ & 3) * IROWS * RB); \
-        _Pragma("unroll") for (int q_ = 0; q_ < CT; ++q_)                             \
-          if (q_ >= g0_ && q_ < g1_) {                                                \
-            const int ct_ = (CT / 2) * (PT) + (q_ >> 1), pp_ = q_ & 1;                \
+        _Pragma("unroll") for (int q_ = 0; q_ < 2 * CT; ++q_)                         \
+          if (!DX_NOW && q_ >= g0_ && q_ < g1_) {                                     \
+            const int ct_ = (EL ? 0 : (CT / 2) * (PT)) + (q_ >> 1), pp_ = q_ & 1;     \
             if constexpr (WB)                                                         \
               AP[2 * ct_ + pp_] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128( \
                   rsy, voy, lofs + (ct_ * KBY + ka_) * 2048 + pp_ * 1024, 0));        \
@@ -393,7 +404,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
           }                                                                           \
         /* CH: the chunk sums of square tile ADDT into mst, 1-2 tiles per chunk */      \
         /* (tile j = 4 ct + board goes with chunk floor(3j / 4)) */                    \
-        if (CH && (ADDT) >= 0) {                                                      \
+        if (CH && !DX_NOADD && (ADDT) >= 0) {                                         \
           const int ja_ = (4 * c_ + 2) / 3, jb_ = ja_ + 1;                            \
           if ((ja_ & 3) < NVB) {                                                      \
             const int ix_ = (ja_ >> 2) * 8 + (ja_ & 3) * 2 + ((ADDT) > 0);            \
@@ -446,7 +457,8 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
 #undef HALF_PINNED
 #undef LOAD_BH
 #undef LOAD_A
-  if (overflow) atomicOr(D.pr.err, ERR_F16);
+  // (the timing-only forms compute garbage that may overflow: no flag from them)
+  if (overflow && !(DX_NOW || DX_NOB || DX_NOADD)) atomicOr(D.pr.err, ERR_F16);
 
   // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
   heads_reduce<NT>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs));
@@ -474,6 +486,24 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
     hipLaunchKernelGGL((k_net_y<S, 114688>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == 4096)
     hipLaunchKernelGGL((k_net_y<S, 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+#ifdef MTAZ_NET_DIAG
+  else if (var == 16384)   // 3-slot weight ring, two k-blocks ahead
+    hipLaunchKernelGGL((k_net_y<S, 16384>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 20))
+    hipLaunchKernelGGL((k_net_y<S, (1 << 20)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 21))
+    hipLaunchKernelGGL((k_net_y<S, (1 << 21)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 22))
+    hipLaunchKernelGGL((k_net_y<S, (1 << 22)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (3 << 20))
+    hipLaunchKernelGGL((k_net_y<S, (3 << 20)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 23))
+    hipLaunchKernelGGL((k_net_y<S, (1 << 23)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 23) + 16384)
+    hipLaunchKernelGGL((k_net_y<S, (1 << 23) + 16384>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (7 << 20))
+    hipLaunchKernelGGL((k_net_y<S, (7 << 20)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+#endif
 
   else
     hipLaunchKernelGGL((k_net_y<S, 0>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);

@@ -74,7 +74,7 @@ for step in "$@"; do
     ab|netab)
       run ab "${AB_TIMEOUT:-400}" python -u tools/bench_net.py ${AB_DIAG:+--diag} --variants "${AB_VARIANTS:-0}" \
         --rounds "${AB_ROUNDS:-4}" --iters "${AB_ITERS:-10}" > "$OUT/ab.json" 2> "$OUT/ab.err"
-      rc=$?; cut -c1-300 "$OUT/ab.json"; tail -3 "$OUT/ab.err"; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+      rc=$?; cut -c1-300 "$OUT/ab.json"; tail -3 "$OUT/ab.err"; if abnormal $rc; then exit $rc; fi ;;
     stress)
       run stress "${STRESS_TIMEOUT:-1000}" python -u tools/train_stress.py ${STRESS_ARGS} > "$OUT/train.jsonl" 2> "$OUT/train.err"
       rc=$?; tail -2 "$OUT/train.jsonl" | cut -c1-600; tail -3 "$OUT/train.err"; if [ $rc -ne 0 ]; then exit $rc; fi ;;
