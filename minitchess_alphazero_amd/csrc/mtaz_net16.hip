@@ -45,6 +45,13 @@ __device__ __forceinline__ float mix_hi(uint32_t pk, float b, float c) {
   return r;
 }
 
+// a * b + c on v_mad_i32_i24 (b uniform; operands within 24 bits signed)
+__device__ __forceinline__ int mad_i24(int a, int b, int c) {
+  int r;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+
 // fp32 add as one v_add_f32 (the compiler would pair adds into v_pk_add_f32, which costs ~13
 // cycles beside MFMAs instead of hiding in their issue gaps: MI355X_MICROARCH.md, cycle constants)
 __device__ __forceinline__ float add_f32(float a, float b) {
@@ -74,6 +81,8 @@ __device__ __forceinline__ void add4(f32x4v& m, const f32x4v& a) {
 // VAR: 0 = product; 1024 = the epilogue in unfused form (bit-identity reference for the
 // product's v_fma_mix epilogue, test_gpu_net.py); 114688 = the K loop without the offset table,
 // the buffer loads and the 2-slot weight ring (bitwise equal, test_y_loop_forms_bit_identical);
+// 16777216 = the row-major swizzled LDS image instead of the chunk-major one (ZL below; bitwise
+// equal, test_y_loop_forms_bit_identical);
 // 4096 (diagnostic library) = one accumulation chain per layer (round 2's k_net_y, see CH below).  Round 1's schedule A/B variants (whole-k-block
 // steps, sched_group_barrier interleaves, 8 waves of 32 channels) measured within 1% of the
 // pinned half-steps and were retired.
@@ -93,7 +102,13 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // half-step ahead) instead of recomputing src_row (~20 VALU / SALU per half-step)
   constexpr bool OT = (VAR & 32768) == 0;
   constexpr int OTB = OT ? 9 * 2 * 64 * 4 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[IMGB + AUXB + OTB];
+  // ZL (product; VAR 1 << 24 = round 2's row-major swizzled image): k_net_z's chunk-major image
+  // (net_common.h zrow / zoff): the bank group of a 16-B cell is its row's, so a 16-lane read group
+  // (16 consecutive output squares, any chunk per lane) is conflict-free, off-board taps included
+  // (a per-lane cell of the board's zero line on the bank the on-board source would have had)
+  constexpr bool ZL = (VAR & (1 << 24)) == 0;
+  constexpr int IMG = ZL ? ZIMGB : IMGB, PART = ZL ? ZPART : PARTB, BSTR = ZL ? ZBOARD : IROWS * RB;
+  __shared__ __attribute__((aligned(16))) char smem[IMG + AUXB + OTB];
   int b0, nb;
   {
     const int n = count ? *count : max_b;
@@ -161,7 +176,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   int xs = 0;
   float mx_img = W.yrange[2 * CONV_LAYERS + 2];   // max |embedding| = max of the stem input
   float mx_blk = 0.f;                             // max of the current residual block's input
-  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMGB + AUXB - 16);
+  unsigned* mxs = reinterpret_cast<unsigned*>(smem + IMG + AUXB - 16);
   if (tid == 0) mxs[0] = mxs[1] = 0u;
   int slot = 0;
 
@@ -199,7 +214,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
         }
         if (pt == 0 || p1 < 30) {
           const int p = pt ? p1 : n;
-          const int ah = ioff(0, bb, p, co0 >> 3) + 8 * (g & 1), al = ah + PARTB;
+          const int ah = (ZL ? zoff(0, bb, p, co0 >> 3) : ioff(0, bb, p, co0 >> 3)) + 8 * (g & 1), al = ah + PART;
           float y[4];
           y[0] = fmaxf(__builtin_fmaf(a[0], in_scale, bv.x), 0.f);
           y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
@@ -259,15 +274,22 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   };
 
   // ---------------- stem: conv3x3 8->256, K = 3 k-blocks of (4 taps x 8 channels) ----------
-  char* simg = smem + IMGB;
-  stem_input<NT>(smem, simg, pos, b0, nb, W, tid);
+  char* simg = smem + IMG;
+  stem_input<NT, ZL>(smem, simg, pos, b0, nb, W, tid);
   if constexpr (OT) {   // entry: row * RB | (g ^ (row & 15)) for square n (tile 0) or 16 + n (tile 1)
     if (wave == 0) {
-      int* ot = reinterpret_cast<int*>(smem + IMGB + AUXB);
+      int* ot = reinterpret_cast<int*>(smem + IMG + AUXB);
       for (int e = 0; e < 18; ++e) {
         const int tap = e >> 1, pt = e & 1;
-        const int r = pt ? src_row(p1, ph1, pw1, tap) : src_row(n, ph0, pw0, tap);
-        ot[e * 64 + lane] = r * RB | (g ^ (r & 15));
+        if constexpr (ZL) {   // chunk g's cell | 1 on the board, the zero-line cell (bit 0 clear) off it
+          const int p = pt ? p1 : n, ph = pt ? ph1 : ph0, pw = pt ? pw1 : pw0;
+          const int dh = tap / 3 - 1, dw = tap % 3 - 1, sq = p + 5 * dh + dw;
+          const bool valid = (p < 30) & ((unsigned)(ph + dh) < 6u) & ((unsigned)(pw + dw) < 5u);
+          ot[e * 64 + lane] = valid ? (zrow(sq, g) | 1) : ZROWS_B + 16 * (sq & 15);
+        } else {
+          const int r = pt ? src_row(p1, ph1, pw1, tap) : src_row(n, ph0, pw0, tap);
+          ot[e * 64 + lane] = r * RB | (g ^ (r & 15));
+        }
       }
     }
   }
@@ -310,7 +332,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // (HALF_PINNED: no accumulator copies, no spills).
   // the weight ring: 2 slots, one k-block ahead (VAR 16384: 3 slots, two ahead, round 2's)
   constexpr int PD = (VAR & 16384) ? 2 : 1, RS = PD + 1, U = CH ? 12 : 6;
-  const char* otab = smem + IMGB + AUXB + 4 * lane;   // OT: this lane's column of the table
+  const char* otab = smem + IMG + AUXB + 4 * lane;   // OT: this lane's column of the table
   int tpre = 0;                                        // OT: the next half-step's table entry
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
   f16x8 A[RS][2 * CT], BH[2][8];
@@ -330,6 +352,16 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)W.convy, (short)0, 0x7ffffff0, 0x00020000);
   const int voy = ((CT * wave) * KBY * 128 + lane) * 16;
   int lofs = 0;   // WB: the layer's byte offset in convy
+  // byte offset (board 0, part 0) of the 16-B chunk ch of the source square of output square p
+  // (row ph, file pw) for tap; off-board / padding: the zero row (ZL: the zero-line cell)
+  auto frag_off = [](int p, int ph, int pw, int tap, int ch) {
+    if constexpr (ZL) {
+      return zsrc(p, ph, pw, tap, ch);
+    } else {
+      const int r = src_row(p, ph, pw, tap);
+      return r * RB + ((ch ^ (r & 15)) << 4);
+    }
+  };
 #define LOAD_A(S, KB)                                                                 \
   {                                                                                   \
     const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
@@ -351,11 +383,10 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   {                                                                                   \
     const int kk_ = (KB) < KBY ? (KB) : KBY - 1;                                      \
     const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                               \
-    const int r_ = (PT) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);   \
-    const int o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                \
+    const int o_ = frag_off((PT) ? p1 : n, (PT) ? ph1 : ph0, (PT) ? pw1 : pw0, tap_, ch_); \
     _Pragma("unroll") for (int part_ = 0; part_ < 2; ++part_)                         \
     _Pragma("unroll") for (int bb_ = 0; bb_ < NVB; ++bb_)                             \
-      S[part_ * 4 + bb_] = *reinterpret_cast<const f16x8*>(smem + part_ * PARTB + bb_ * IROWS * RB + o_); \
+      S[part_ * 4 + bb_] = *reinterpret_cast<const f16x8*>(smem + part_ * PART + bb_ * BSTR + o_); \
   }
 // product half-step: 12 chunks of 4 MFMAs in fixed program order (sched_barrier between
 // chunks), LDS reads 2 per chunk in chunks 0-3, weight loads 1 per chunk in chunks 4-7
@@ -365,16 +396,20 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
     int o_;                                                                           \
     if constexpr (OT) {                                                               \
       /* tpre holds the entry of (KBN, PTN); load the one of (KB + 1, PT) for the next half */ \
-      const int t_ = tpre, x_ = t_ ^ (4 * (kk_ & 7));                                 \
-      o_ = (t_ & ~31) | ((x_ & 31) << 4);                                             \
+      if constexpr (ZL) {                                                             \
+        /* on the board: entry = cell | 1, + 1024 (kk & 7) - 1; off: the entry (bit 0 clear) */ \
+        o_ = mad_i24(tpre & 1, 1024 * (kk_ & 7) - 1, tpre);                             \
+      } else {                                                                        \
+        const int t_ = tpre, x_ = t_ ^ (4 * (kk_ & 7));                               \
+        o_ = (t_ & ~31) | ((x_ & 31) << 4);                                           \
+      }                                                                               \
       const int kq_ = ((KB) + 1) < KBY ? ((KB) + 1) : KBY - 1;                        \
       tpre = *reinterpret_cast<const int*>(otab + ((kq_ >> 3) * 2 + (PT)) * 256);     \
     } else {                                                                          \
       const int tap_ = kk_ >> 3, ch_ = 4 * (kk_ & 7) + g;                             \
-      const int r_ = (PTN) ? src_row(p1, ph1, pw1, tap_) : src_row(n, ph0, pw0, tap_);\
-      o_ = r_ * RB + ((ch_ ^ (r_ & 15)) << 4);                                        \
+      o_ = frag_off((PTN) ? p1 : n, (PTN) ? ph1 : ph0, (PTN) ? pw1 : pw0, tap_, ch_);  \
     }                                                                                 \
-    const int o1_ = o_ + PARTB;                                                       \
+    const int o1_ = o_ + PART;                                                        \
     const int ka_ = ((KB) + PD) < KBY ? ((KB) + PD) : KBY - 1;                        \
     const uint4* pa_ = Wl + (size_t)ka_ * 128;                                        \
     _Pragma("unroll") for (int i_ = 0; i_ < 12 * CT; ++i_) {                          \
@@ -389,10 +424,10 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
                            : ((c_ >= 4 && c_ < 4 + CT) ? c_ - 4 : 0);                 \
         const int g1_ = EL ? (((PT) == 0 && c_ >= 1 && c_ <= 2 * CT) ? c_ : 0)         \
                            : ((c_ >= 4 && c_ < 4 + CT) ? c_ - 3 : 0);                 \
-        /* part 1 from its own base (o_ + PARTB): the board offsets stay 16-bit immediates */ \
+        /* part 1 from its own base (o_ + PART): the board offsets stay 16-bit immediates */ \
         _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_)                              \
           if (!DX_NOB && q_ >= l0_ && q_ < l1_ && (q_ & 3) < NVB)                     \
-            BN[q_] = *reinterpret_cast<const f16x8*>(smem + ((q_ >> 2) ? o1_ : o_) + (q_ & 3) * IROWS * RB); \
+            BN[q_] = *reinterpret_cast<const f16x8*>(smem + ((q_ >> 2) ? o1_ : o_) + (q_ & 3) * BSTR); \
         _Pragma("unroll") for (int q_ = 0; q_ < 2 * CT; ++q_)                         \
           if (!DX_NOW && q_ >= g0_ && q_ < g1_) {                                     \
             const int ct_ = (EL ? 0 : (CT / 2) * (PT)) + (q_ >> 1), pp_ = q_ & 1;     \
@@ -428,8 +463,9 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   }
   for (int L = 0; L < CONV_LAYERS; ++L) {
 #pragma unroll
-    for (int p = 0; p < PD; ++p) LOAD_A(A[p], p);
+    for (int p = 0; p < (DX_NOW ? RS : PD); ++p) LOAD_A(A[p], p);   // (DX_NOW: every slot defined once)
     LOAD_BH(BH[0], 0, 0);
+    if constexpr (DX_NOB) LOAD_BH(BH[1], 0, 1);
     if constexpr (OT) tpre = *reinterpret_cast<const int*>(otab + 1 * 256);   // (k-block 0, tile 1)
     for (int kb = 0; kb < KBY; kb += U) {
 #pragma unroll
@@ -461,7 +497,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   if (overflow && !(DX_NOW || DX_NOB || DX_NOADD)) atomicOr(D.pr.err, ERR_F16);
 
   // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
-  heads_reduce<NT>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs));
+  heads_reduce<NT, false, ZL>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs));
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
@@ -473,7 +509,7 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
       stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
     }
   }
-  heads_out(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
+  heads_out<ZL>(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
 }
 
 template <bool S>
@@ -486,6 +522,8 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
     hipLaunchKernelGGL((k_net_y<S, 114688>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == 4096)
     hipLaunchKernelGGL((k_net_y<S, 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 24))   // the row-major swizzled image of rounds 1-3 (bit identity, A/B)
+    hipLaunchKernelGGL((k_net_y<S, (1 << 24)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
 #ifdef MTAZ_NET_DIAG
   else if (var == 16384)   // 3-slot weight ring, two k-blocks ahead
     hipLaunchKernelGGL((k_net_y<S, 16384>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
@@ -497,6 +535,12 @@ static void launch_y(int var, dim3 grid, hipStream_t s, const Dev& d, const NetW
     hipLaunchKernelGGL((k_net_y<S, (1 << 22)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == (3 << 20))
     hipLaunchKernelGGL((k_net_y<S, (3 << 20)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 20) + 4096)
+    hipLaunchKernelGGL((k_net_y<S, (1 << 20) + 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (1 << 21) + 4096)
+    hipLaunchKernelGGL((k_net_y<S, (1 << 21) + 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
+  else if (var == (3 << 20) + 4096)
+    hipLaunchKernelGGL((k_net_y<S, (3 << 20) + 4096>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == (1 << 23))
     hipLaunchKernelGGL((k_net_y<S, (1 << 23)>), grid, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits, values, stamps, 0);
   else if (var == (1 << 23) + 16384)

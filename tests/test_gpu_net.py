@@ -117,7 +117,8 @@ def test_product_library_rejects_untested_variants():
     eng = Engine(n_games=4, sims=2)
     for prec, good, bad in (('f16f8', [0, 1, 8192, 2097152, 25165824, 33554432, 58720256],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
-                            ('f16x3', [0, 1, 1024, 114688], [512, 4, 8, 2048, 8192, 4096, 268435456, 16384, 32768])):
+                            ('f16x3', [0, 1, 1024, 114688, 16777216],
+                             [512, 4, 8, 2048, 8192, 4096, 268435456, 16384, 32768])):
         eng.set_precision(prec)
         for v in good:
             eng.set_net_variant(v)
@@ -178,10 +179,11 @@ def test_z_loop_forms_bit_identical():
 
 def test_y_loop_forms_bit_identical():
     """k_net_y's K loop with the LDS offset table, buffer-loaded weights and the 2-slot weight ring
-    (the product) computes exactly the loop before them (variant 114688): logits and values bitwise
-    equal on an ordinary, a wide-range and a tiny-activation net.  1024 boards = one full round of
-    4 boards per workgroup on 256 CUs, so both builds group the boards alike (variant 114688 has no
-    tail launches)."""
+    (the product) computes exactly the loop before them (variant 114688), and the chunk-major LDS
+    image exactly the row-major swizzled one of rounds 1-3 (variant 16777216): logits and values
+    bitwise equal on an ordinary, a wide-range and a tiny-activation net.  1024 boards = one full
+    round of 4 boards per workgroup on 256 CUs, so the builds group the boards alike (the variants
+    have no tail launches)."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from minitchess_alphazero_amd.network import Network
@@ -195,10 +197,11 @@ def test_y_loop_forms_bit_identical():
         eng.set_weights(net)
         eng.set_net_variant(0)
         l0, v0 = eng.evaluate(pos)
-        eng.set_net_variant(114688)
-        l1, v1 = eng.evaluate(pos)
-        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
-        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+        for var in (114688, 16777216):
+            eng.set_net_variant(var)
+            l1, v1 = eng.evaluate(pos)
+            assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), var
+            assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), var
 
 
 @pytest.mark.parametrize('precision', ['f16f8', 'f16x3'])
