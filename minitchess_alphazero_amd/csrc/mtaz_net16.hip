@@ -212,7 +212,12 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
             acc_t = (f32x4v){0};
           }
         }
-        if (pt == 0 || p1 < 30) {
+        // ZL: the padding squares 30, 31 of square tile 1 are computed and stored like the others,
+        // without a lane-divergent branch: their cells (rows 30, 31 of the chunk-major image) are
+        // never a fragment source (off-board taps read the zero line), nor read by the heads, and
+        // their values stay out of the workgroup max
+        const bool real = pt == 0 || p1 < 30;
+        if (ZL || real) {
           const int p = pt ? p1 : n;
           const int ah = (ZL ? zoff(0, bb, p, co0 >> 3) : ioff(0, bb, p, co0 >> 3)) + 8 * (g & 1), al = ah + PART;
           float y[4];
@@ -220,7 +225,8 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
           y[1] = fmaxf(__builtin_fmaf(a[1], in_scale, bv.y), 0.f);
           y[2] = fmaxf(__builtin_fmaf(a[2], in_scale, bv.z), 0.f);
           y[3] = fmaxf(__builtin_fmaf(a[3], in_scale, bv.w), 0.f);
-          ymax = fmaxf(fmaxf(ymax, fmaxf(y[0], y[1])), fmaxf(y[2], y[3]));   // stored units
+          const float ym = fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3]));
+          ymax = real ? fmaxf(ymax, ym) : ymax;   // stored units
           if constexpr (VAR & 1024) {   // reference form of the same epilogue (unfused)
             if constexpr (conv_a) {
               const f16x4 xh = *reinterpret_cast<const f16x4*>(smem + ah);
