@@ -336,8 +336,11 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // activation fragments of one tile are live (a 2 x 8-fragment ring): the next half's are read
   // from LDS during the current half, in 12 chunks of 4 MFMAs whose order sched_barrier pins
   // (HALF_PINNED: no accumulator copies, no spills).
-  // the weight ring: 2 slots, one k-block ahead (VAR 16384: 3 slots, two ahead, round 2's)
-  constexpr int PD = (VAR & 16384) ? 2 : 1, RS = PD + 1, U = CH ? 12 : 6;
+  // the weight ring: 2 slots, one k-block ahead (VAR 16384: 3 slots, two ahead, round 2's; tail
+  // instances: below)
+  // Tail instances prefetch deeper: with 1 or 2 boards a k-block is 384 or 768 MFMA cycles, less
+  // than an L2 round trip under load, and they have registers to spare (1 board: 200 of 512)
+  constexpr int PD = (VAR & 16384) ? 2 : NVB == 1 ? 3 : NVB == 2 ? 2 : 1, RS = PD + 1, U = CH ? 12 : 6;
   const char* otab = smem + IMG + AUXB + 4 * lane;   // OT: this lane's column of the table
   int tpre = 0;                                        // OT: the next half-step's table entry
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
