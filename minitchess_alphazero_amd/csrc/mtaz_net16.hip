@@ -91,11 +91,18 @@ __device__ __forceinline__ void add4(f32x4v& m, const f32x4v& a) {
 // the remaining boards, at most NVB per workgroup, computing only those (boards NVB..3 of the
 // image are never computed).  The workgroup's stored-units exponent xs follows the bound of its
 // own boards, so the assignment is exact for any net whose activations stay below 2^14 (xs = 0).
+// LDS bytes of a VAR build: the image, the aux region, the fragment offset table
+constexpr int net_y_smem(int var) {
+  return ((var & (1 << 24)) ? IMGB : ZIMGB) + AUXB + ((var & 32768) ? 0 : 9 * 2 * 64 * 4);
+}
+
+// the network on workgroup `bid`'s boards (k_net_y, k_net_y_tail below), in the kernel's LDS `smem`
 template <bool STAMP, int VAR, int NVB = XB>
-__global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
-                                                  const int32_t* __restrict__ count, int max_b, int mode,
-                                                  float* __restrict__ logits_out, float* __restrict__ values_out,
-                                                  unsigned long long* __restrict__ stamps, int ncu) {
+__device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev& D, const NetWeights& W,
+                                           const Pos* __restrict__ pos, const int32_t* __restrict__ count,
+                                           int max_b, int mode, float* __restrict__ logits_out,
+                                           float* __restrict__ values_out, unsigned long long* __restrict__ stamps,
+                                           int ncu) {
   static_assert(NVB >= 1 && NVB <= XB, "boards per workgroup");
   // OT (product; VAR 32768 = off): the K loop's fragment offsets come from a per-lane LDS table of
   // the source rows [tap 9][square tile 2][lane 64] (one ds_read_b32 per half-step, issued a
@@ -108,17 +115,17 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   // (a per-lane cell of the board's zero line on the bank the on-board source would have had)
   constexpr bool ZL = (VAR & (1 << 24)) == 0;
   constexpr int IMG = ZL ? ZIMGB : IMGB, PART = ZL ? ZPART : PARTB, BSTR = ZL ? ZBOARD : IROWS * RB;
-  __shared__ __attribute__((aligned(16))) char smem[IMG + AUXB + OTB];
+  static_assert(IMG + AUXB + OTB == net_y_smem(VAR), "LDS layout");
   int b0, nb;
   {
     const int n = count ? *count : max_b;
     const int r = ncu > 0 ? n % (XB * ncu) : 0, per = ncu > 0 ? (r + ncu - 1) / ncu : XB;
     if constexpr (NVB == XB) {   // the full rounds (and a tail of 4 boards per CU)
-      b0 = blockIdx.x * XB;
+      b0 = bid * XB;
       nb = per < XB ? n - r : n;
     } else {                     // the tail, when it has NVB boards per CU
       if (per != NVB) return;
-      b0 = n - r + blockIdx.x * NVB;
+      b0 = n - r + bid * NVB;
       nb = b0 + NVB < n ? b0 + NVB : n;
     }
   }
@@ -510,15 +517,42 @@ __global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos
   stamp(st_heads);
   if constexpr (STAMP) {
     if (tid == 0) {
-      stamps[blockIdx.x * 6 + 0] = st_stem;
-      stamps[blockIdx.x * 6 + 1] = st_k;
-      stamps[blockIdx.x * 6 + 2] = st_epi;
-      stamps[blockIdx.x * 6 + 3] = st_heads;
-      stamps[blockIdx.x * 6 + 4] = __builtin_amdgcn_s_memtime() - t_start;
-      stamps[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
+      stamps[bid * 6 + 0] = st_stem;
+      stamps[bid * 6 + 1] = st_k;
+      stamps[bid * 6 + 2] = st_epi;
+      stamps[bid * 6 + 3] = st_heads;
+      stamps[bid * 6 + 4] = __builtin_amdgcn_s_memtime() - t_start;
+      stamps[bid * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
     }
   }
   heads_out<ZL>(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
+}
+
+template <bool STAMP, int VAR, int NVB = XB>
+__global__ __launch_bounds__(256, 1) void k_net_y(Dev D, NetWeights W, const Pos* __restrict__ pos,
+                                                  const int32_t* __restrict__ count, int max_b, int mode,
+                                                  float* __restrict__ logits_out, float* __restrict__ values_out,
+                                                  unsigned long long* __restrict__ stamps, int ncu) {
+  __shared__ __attribute__((aligned(16))) char smem[net_y_smem(VAR)];
+  net_y_body<STAMP, VAR, NVB>(smem, blockIdx.x, D, W, pos, count, max_b, mode, logits_out, values_out, stamps, ncu);
+}
+
+// The three tail instances in one launch of 3 x ncu workgroups: workgroup i runs as the
+// (1 + i / ncu)-board instance for CU slot i % ncu, and exits at once unless the remainder has that
+// many boards per CU (one launch instead of three, two of which were always empty)
+template <int VAR>
+__global__ __launch_bounds__(256, 1) void k_net_y_tail(Dev D, NetWeights W, const Pos* __restrict__ pos,
+                                                       const int32_t* __restrict__ count, int max_b, int mode,
+                                                       float* __restrict__ logits_out,
+                                                       float* __restrict__ values_out, int ncu) {
+  __shared__ __attribute__((aligned(16))) char smem[net_y_smem(VAR)];
+  const int nvb = 1 + (int)blockIdx.x / ncu, bid = (int)blockIdx.x % ncu;
+  if (nvb == 1)
+    net_y_body<false, VAR, 1>(smem, bid, D, W, pos, count, max_b, mode, logits_out, values_out, nullptr, ncu);
+  else if (nvb == 2)
+    net_y_body<false, VAR, 2>(smem, bid, D, W, pos, count, max_b, mode, logits_out, values_out, nullptr, ncu);
+  else
+    net_y_body<false, VAR, 3>(smem, bid, D, W, pos, count, max_b, mode, logits_out, values_out, nullptr, ncu);
 }
 
 template <bool S>
@@ -583,12 +617,8 @@ void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const i
   if (variant == 0 && ncu > 0) {   // the product: full rounds, then the tail launches (k_net_y above)
     hipLaunchKernelGGL((k_net_y<false, 0, XB>), dim3((max_b + XB - 1) / XB), dim3(256), 0, s, d, w, pos, count, max_b,
                        mode, logits_out, values_out, nullptr, ncu);
-    hipLaunchKernelGGL((k_net_y<false, 0, 1>), dim3(ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
-                       values_out, nullptr, ncu);
-    hipLaunchKernelGGL((k_net_y<false, 0, 2>), dim3(ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
-                       values_out, nullptr, ncu);
-    hipLaunchKernelGGL((k_net_y<false, 0, 3>), dim3(ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
-                       values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_y_tail<0>), dim3(3 * ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, ncu);
   } else {   // variant 1: 4 boards per workgroup throughout
     launch_y<false>(variant == 1 ? 0 : variant, dim3((max_b + XB - 1) / XB), s, d, w, pos, count, max_b, mode,
                     logits_out, values_out, nullptr);

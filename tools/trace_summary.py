@@ -23,7 +23,7 @@ def main():
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    net = re.compile(r'void mtaz::(k_net_[yz])<false, \d+, (\d)>')
+    net = re.compile(r'void mtaz::(k_net_[yz])(?:<false, \d+, (\d)>|_tail<\d+>)')
     steps = []        # [(build, [evaluation dicts])]
     tails = collections.defaultdict(list)
     gaps = collections.defaultdict(list)
@@ -37,7 +37,7 @@ def main():
         m = net.match(name)
         if not m:
             continue
-        build, nvb = m.group(1), int(m.group(2))
+        build, nvb = m.group(1), int(m.group(2) or 0)   # 0: k_net_y_tail (the three tail instances)
         dur = (en - st) / 1e3
         if nvb == 4:
             if int(r['Grid_Size_X']) < 256 * 64:    # evaluate() of a few positions (code object load)
@@ -47,7 +47,7 @@ def main():
             steps[-1][1].append({'main': dur, 'tails': 0.0})
         elif steps and steps[-1][0] == build and steps[-1][1]:
             steps[-1][1][-1]['tails'] += dur
-            tails[f'{build}<{nvb}>'].append(dur)
+            tails[f'{build}<{nvb}>' if nvb else f'{build}_tail'].append(dur)
     out = {'steps': [], 'tail_instances': {}, 'gap_median_us': {}}
     for build, ev in steps:
         n = len(ev)
