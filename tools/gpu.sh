@@ -10,7 +10,9 @@
 #   tests            pytest -m gpu (K_EXPR: a -k filter, PYTEST_FILES: files instead of tests/)
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py $BENCH_ARGS           -> bench.json (the JSON line), bench.err
-#   prof             rocprofv3 --kernel-trace --stats of bench.py $PROF_ARGS (default: --no-cpu-baseline)
+#   prof             rocprofv3 --kernel-trace --stats of bench.py $PROF_ARGS (default: --no-cpu-baseline);
+#                    per-evaluation main / tail / gap summary: python tools/trace_summary.py
+#                    gpurun_out/OUT/prof/bench_kernel_trace.csv
 #   pmc              rocprofv3 --pmc passes on the network kernel, one counter group per pass
 #                    (FETCH_SIZE / WRITE_SIZE / TCC hit-miss / SQ busy group), of bench.py $PMC_ARGS;
 #                    summarise with python tools/pmc_summary.py gpurun_out/OUT/pmc
