@@ -345,9 +345,10 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   // (HALF_PINNED: no accumulator copies, no spills).
   // the weight ring: 2 slots, one k-block ahead (VAR 16384: 3 slots, two ahead, round 2's; tail
   // instances: below)
-  // Tail instances prefetch deeper: with 1 or 2 boards a k-block is 384 or 768 MFMA cycles, less
-  // than an L2 round trip under load, and they have registers to spare (1 board: 200 of 512)
-  constexpr int PD = (VAR & 16384) ? 2 : NVB == 1 ? 3 : NVB == 2 ? 2 : 1, RS = PD + 1, U = CH ? 12 : 6;
+  // Tail instances prefetch deeper: with 1, 2 or 3 boards a k-block is 384, 768 or 1,152 MFMA
+  // cycles, less than an L2 round trip under load, and they have registers to spare (1 board: 200
+  // of 512 with the 2-slot ring)
+  constexpr int PD = (VAR & 16384) ? 2 : NVB == 1 ? 5 : NVB == 2 ? 3 : NVB == 3 ? 2 : 1, RS = PD + 1, U = CH ? 12 : 6;
   const char* otab = smem + IMG + AUXB + 4 * lane;   // OT: this lane's column of the table
   int tpre = 0;                                        // OT: the next half-step's table entry
   static_assert(KBY % U == 0 && U % RS == 0 && RS > PD, "ring");
