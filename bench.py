@@ -17,6 +17,7 @@ import os
 import sys
 import time
 
+T_START = time.time()                # the budget clock (--time-budget) starts with the process
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
@@ -35,6 +36,11 @@ PRECISION_NOTE = {
     0: 'fp32: fp32 MFMA trunk (k_conv3x3)',
 }
 TREE_BYTES_PER_SIM = 700             # SURVEY 8d algorithmic bytes per simulation of the tree walk
+
+
+def elapsed():
+    """Seconds since this process started (the driver's own clock starts a little earlier)."""
+    return time.time() - T_START
 
 
 def log(msg):
@@ -79,18 +85,25 @@ def host_cores():
             'usable': usable}
 
 
-def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=()):
+def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budget=None):
     """seeded games (np.random.seed(g), random-init weights) at C1's 32 sims,
     the repo's default 36 (app/base.py:25) and the GPU's sims per move, each on all cores (games one
     after another, torch.set_num_threads = all_threads) and on 1 thread (all single-thread games at
     once, one process each: every game still runs alone on one core).  Children are separate
-    processes (spawned, never exec'ed over this one) and touch no GPU.  value = games/s at the
-    GPU's sims on all cores."""
+    processes (spawned, never exec'ed over this one) and touch no GPU; nothing else runs meanwhile.
+    value = games/s at the GPU's sims on all cores.
+
+    The legs run in priority order, each only when its estimate (scaled from the first leg's
+    seconds per game) ends before `deadline` (s since process start): the GPU's sims on all cores
+    (the value), the other sims on all cores, then the 1-thread legs (all at once).  Skipped legs
+    are named in budget['skipped'], never silently dropped."""
     import multiprocessing as mp
     seeds = [0, 1, 2] if plan == 'full' else [0]
-    sims_list = sorted({32, gpu_sims, *extra_sims}) if plan == 'full' else sorted({gpu_sims, *extra_sims})
+    others = sorted({32, *extra_sims} - {gpu_sims}, reverse=True) if plan == 'full' else sorted(set(extra_sims) - {gpu_sims})
+    sims_list = sorted({gpu_sims, *others})
     ctx = mp.get_context('spawn')
     runs = {}
+    skipped = budget['skipped'] if budget is not None else []
 
     def record(sims, label, thr, games):
         secs = [g['seconds'] for g in games]
@@ -101,19 +114,35 @@ def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=()):
             'nn_evals': [g['nn_evals'] for g in games],
             'sims_per_s': sum(g['plies'] for g in games) * sims / sum(secs)}
 
-    if plan == 'full':
-        # 1 thread: every (sims, seed) game at once, one single-threaded process each (6 of the
-        # host's cores, each game alone on its core)
-        jobs = [(sims, sd, 1) for sims in sims_list for sd in seeds]
-        with ctx.Pool(len(jobs)) as pool:
-            out = pool.map(_cpu_game, jobs, chunksize=1)
-        for i, sims in enumerate(sims_list):
-            record(sims, '1thread', 1, out[i * len(seeds):(i + 1) * len(seeds)])
-    # all cores: the games one after another in one process
-    for sims in sims_list:
+    def fits(label, est):
+        if deadline is None or elapsed() + est <= deadline:
+            return True
+        skipped.append({'leg': f'cpu baseline {label}', 'estimate_s': round(est, 1)})
+        log(f'BUDGET: skipping cpu baseline {label} (~{est:.0f} s; {elapsed():.0f} s used of {deadline:.0f} s)')
+        return False
+
+    def all_cores(sims):
         with ctx.Pool(1) as pool:
-            record(sims, 'all', all_threads, pool.map(_cpu_game, [(sims, sd, all_threads) for sd in seeds],
-                                                      chunksize=1))
+            record(sims, 'all', all_threads, pool.map(_cpu_game, [(sims, sd, all_threads) for sd in seeds], chunksize=1))
+
+    # the value leg: the GPU's sims on all cores (its own estimate: ~0.35 s per sim per game on 16
+    # cores, measured rounds 1-3)
+    if not fits(f'{gpu_sims} sims all cores', len(seeds) * 0.35 * gpu_sims * 16 / max(1, all_threads) + 5):
+        return None
+    all_cores(gpu_sims)
+    per_sim = sum(runs[f'{gpu_sims}sims/all']['seconds_per_game']) / len(seeds) / gpu_sims   # s per game per sim
+    for sims in others:
+        if fits(f'{sims} sims all cores', len(seeds) * per_sim * sims * 1.25 + 5):
+            all_cores(sims)
+    if plan == 'full':
+        # 1 thread: every (sims, seed) game at once, one single-threaded process each (each game alone
+        # on its core; measured at ~2.4x the all-core seconds per game)
+        if fits('1-thread legs', per_sim * max(sims_list) * 2.6 * 1.2 + 8):
+            jobs = [(sm, sd, 1) for sm in sims_list for sd in seeds]
+            with ctx.Pool(len(jobs)) as pool:
+                out = pool.map(_cpu_game, jobs, chunksize=1)
+            for i, sm in enumerate(sims_list):
+                record(sm, '1thread', 1, out[i * len(seeds):(i + 1) * len(seeds)])
     head = runs[f'{gpu_sims}sims/all']
     return {'value': head['games_per_s'], 'unit': 'games/s', 'cores': all_threads, 'kind': 'port',
             'sample': (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
@@ -173,9 +202,18 @@ def main():
     ap.add_argument('--cpu-plan', default='full', choices=['full', 'quick'],
                     help='full: BASELINE.md section 4 (3 seeded games x {32, --sims} sims x {all cores, 1 thread}); '
                          'quick: 1 game at --sims on all cores')
-    ap.add_argument('--no-secondary', action='store_true',
-                    help='skip the second timed step with the other fused network (k_net_z when the main '
-                         'line runs k_net_y and vice versa)')
+    ap.add_argument('--secondary', action='store_true',
+                    help='one more timed step with the other fused network (k_net_z when the main line runs '
+                         'k_net_y): an A/B outside the 1e-5 contract on the stress net, off by default')
+    ap.add_argument('--no-secondary', action='store_true', help=argparse.SUPPRESS)   # (the default now)
+    ap.add_argument('--host-threads', type=int, default=0,
+                    help="host threads of the engine's per-move work (Dirichlet draws, action choice); 0 = this "
+                         "rank's share of the usable cores (launch.rank_host_share), at most 16")
+    ap.add_argument('--time-budget', type=float, default=float(os.environ.get('MTAZ_BENCH_BUDGET_S', 500)),
+                    help='wall-clock budget in s from process start (the driver kills the run at 600 s): the '
+                         'timed steps must fit (else exit 3 with a message before timing); the optional legs '
+                         '(36-sims step, CPU baseline runs) are skipped, and named in the JSON, when they '
+                         'would not')
     ap.add_argument('--default-sims', type=int, default=36,
                     help="one more timed step at the repo's default sims per move (app/base.py:25: 36; 0 = skip), "
                          'reported with its CPU baseline as at_repo_default_sims')
@@ -250,17 +288,43 @@ def main():
     else:
         torch.manual_seed(0)                      # random-init weights of the reference architecture
         net_for_engine = Network()
+    eng_threads = args.host_threads or min(16, host_threads)
     eng.set_weights(net_for_engine)
     eng.set_memo(args.memo)
-    eng.set_host_threads(min(16, host_threads))
+    eng.set_host_threads(eng_threads)
     eng.set_precision(args.precision)
     eng.set_net_variant(args.net_variant)
     eng.set_timing(True)
     eng.set_pipeline(args.groups)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
+
+    def agree_max(x):
+        """The max of x over ranks (budget decisions must be the same on every rank)."""
+        if dist is None:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64, device=red_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    warm_s = []
     for i in range(args.warmup):
+        t0 = time.perf_counter()
         eng.play()
-        log(f'warmup {i + 1}/{args.warmup}')
+        warm_s.append(time.perf_counter() - t0)
+        log(f'warmup {i + 1}/{args.warmup}: {warm_s[-1]:.2f} s')
+    budget = {'limit_s': args.time_budget, 'skipped': []}
+    if warm_s:
+        # the timed steps are the contract: if they cannot fit the budget, say so and stop before
+        # timing rather than being killed without a line
+        step_est = agree_max(sum(warm_s[1:] or warm_s) / len(warm_s[1:] or warm_s))
+        need = elapsed() + args.steps * step_est
+        budget['main_projected_end_s'] = round(need, 1)
+        if need > args.time_budget:
+            log(f'BUDGET: {args.steps} steps of ~{step_est:.1f} s would end at {need:.0f} s, past the '
+                f'{args.time_budget:.0f} s budget (--time-budget); stopping before the timed region')
+            if dist is not None:
+                dist.destroy_process_group()
+            sys.exit(3)
 
     def sync():
         torch.cuda.synchronize(device)
@@ -302,25 +366,22 @@ def main():
 
     dt, tot, prec = timed(eng, args.steps, 'main')
     games = G * args.steps * world
+    step_s = dt / args.steps
 
-    # secondary line: one more timed step on the other fused network (k_net_z, f16f8, when the main
-    # line runs k_net_y), same engine, seeds and workload, so both builds' throughput comes from one
-    # run.  k_net_z's tested scope is narrower: within 1e-5 on the seed-0 and
-    # C3 nets, not on the round-3 stress net
-    secondary = None
-    other = {'f16x3': 'f16f8', 'f16f8': 'f16x3'}.get(args.precision)
-    if not args.no_secondary and other:
-        eng.set_precision(other)
-        eng.evaluate(np.stack([start_position()] * 8))    # load the other build's code objects
-        dt2, tot2, prec2 = timed(eng, 1, f'secondary ({other})')
-        eng.set_precision(args.precision)
-        secondary = {'precision': PRECISION_NOTE[prec2], 'value': G * world / dt2, 'unit': 'games/s', 'steps': 1,
-                     'ms_per_step': dt2 * 1e3, 'roofline': kernel_roofline(tot2, prec2), **counters(tot2, dt2, G * world)}
+    def fits(label, est_s):
+        """True when an optional leg of ~est_s seconds ends inside the budget (same answer on every
+        rank); otherwise it is named in the JSON line's budget.skipped."""
+        ok = agree_max(elapsed() + est_s) <= args.time_budget
+        if not ok:
+            budget['skipped'].append({'leg': label, 'estimate_s': round(est_s, 1)})
+            log(f'BUDGET: skipping {label} (~{est_s:.0f} s; {elapsed():.0f} s of {args.time_budget:.0f} s used)')
+        return ok
 
     # the north_star's measurement point: the repo's default sims per move (app/base.py:25), same
     # games, seeds, weights and precision as the main line
     at_default = None
-    if args.default_sims and args.default_sims != sims:
+    if args.default_sims and args.default_sims != sims and fits(f'{args.default_sims}-sims step',
+                                                                 step_s * args.default_sims / sims * 1.15 + 5):
         eng36 = Engine(n_games=G, sims=args.default_sims, device=device, seed_base=seed_base)
         eng36.set_weights(net_for_engine)
         eng36.set_precision(args.precision)
@@ -328,12 +389,25 @@ def main():
         eng36.set_timing(True)
         eng36.set_pipeline(args.groups)
         eng36.set_memo(args.memo)
-        eng36.set_host_threads(min(16, host_threads))
+        eng36.set_host_threads(eng_threads)
         eng36.evaluate(np.stack([start_position()] * 8))
         dt3, tot3, prec3 = timed(eng36, 1, f'{args.default_sims} sims')
         at_default = {'sims_per_move': args.default_sims, 'value': G * world / dt3, 'unit': 'games/s', 'steps': 1,
                       'ms_per_step': dt3 * 1e3, 'roofline': kernel_roofline(tot3, prec3), **counters(tot3, dt3, G * world)}
         eng36.close()
+
+    # secondary line (opt-in, --secondary): one more timed step on the other fused network (k_net_z,
+    # f16f8, when the main line runs k_net_y), same engine, seeds and workload.  k_net_z's tested scope
+    # is narrower: within 1e-5 on the seed-0 and C3 nets, not on the stress net
+    secondary = None
+    other = {'f16x3': 'f16f8', 'f16f8': 'f16x3'}.get(args.precision)
+    if args.secondary and other and fits(f'secondary ({other})', step_s + 5):
+        eng.set_precision(other)
+        eng.evaluate(np.stack([start_position()] * 8))    # load the other build's code objects
+        dt2, tot2, prec2 = timed(eng, 1, f'secondary ({other})')
+        eng.set_precision(args.precision)
+        secondary = {'precision': PRECISION_NOTE[prec2], 'value': G * world / dt2, 'unit': 'games/s', 'steps': 1,
+                     'ms_per_step': dt2 * 1e3, 'roofline': kernel_roofline(tot2, prec2), **counters(tot2, dt2, G * world)}
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -384,6 +458,7 @@ def main():
                           # k_leaf_compact (the leaf list in game order, one workgroup) follows every
                           # k_select launch; its time is outside the k_select roofline
                           'leaf_compact_avg_ms': tot['compact_ms'] / tot['waves'] if tot['waves'] else None},
+        'host_threads': eng_threads,
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
         # host time between two moves' simulations (the GPU idles): action choice + records
@@ -398,14 +473,18 @@ def main():
     line['host_cores'] = host_cores()
     if world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or line['host_cores']['usable']
-        extra = (args.default_sims,) if at_default is not None else ()
-        line['cpu_baseline'] = cpu_baseline(args.cpu_plan, threads, sims, extra)
-        line['vs_cpu_baseline'] = line['value'] / line['cpu_baseline']['value']
-        if at_default is not None:
-            r36 = line['cpu_baseline']['runs'][f'{args.default_sims}sims/all']
-            at_default['cpu_baseline_games_per_s'] = r36['games_per_s']
-            at_default['cpu_baseline_sims_per_s'] = r36['sims_per_s']
-            at_default['vs_cpu_baseline'] = at_default['value'] / r36['games_per_s']
+        extra = (args.default_sims,) if args.default_sims and args.default_sims != sims else ()
+        cb = cpu_baseline(args.cpu_plan, threads, sims, extra, deadline=args.time_budget, budget=budget)
+        if cb is not None:
+            line['cpu_baseline'] = cb
+            line['vs_cpu_baseline'] = line['value'] / cb['value']
+            r36 = cb['runs'].get(f'{args.default_sims}sims/all')
+            if at_default is not None and r36 is not None:
+                at_default['cpu_baseline_games_per_s'] = r36['games_per_s']
+                at_default['cpu_baseline_sims_per_s'] = r36['sims_per_s']
+                at_default['vs_cpu_baseline'] = at_default['value'] / r36['games_per_s']
+    budget['end_s'] = round(elapsed(), 1)
+    line['budget'] = budget
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -32,6 +32,7 @@ SOURCES = [
     # (16K) the tail instantiations (fewer boards) were left rolled, and their accumulator arrays
     # went to scratch (round 3: k_net_y<., ., 3> 14x slower)
     ('mtaz_net16.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
+    ('mtaz_net16_r3.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
     ('mtaz_net8.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
     ('mtaz_wire.cpp', ['-O2']),

@@ -171,6 +171,10 @@ struct NetWeights {
   const float* convx_inv; // [18] 2^-e_L
   const float* stemx_inv; // [1] the stem's
   const uint4* convy;
+  // round 4's k_net_y: the same split weights k-block-major, [L 18][kblock 72][cotile 16][part]
+  // [lane 64][8 x f16], so that one k-block's 8 fragments of a wave sit at one scalar base plus
+  // immediates (buffer loads with no per-load scalar arithmetic)
+  const uint4* convyk;
   // stem: [cotile 16][kblock 3][part][lane 64][8 x f16], co = 16*cotile + (l&15),
   // tap = 4*kblock + (l>>4) (taps 9..11 zero), channel j; scale stemx_inv
   const uint4* stemy;
@@ -241,6 +245,10 @@ void launch_net(const Dev& d, const NetWeights& w, const NetBuffers& nb, const P
 void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
                       float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
                       int variant);
+// round 3's k_net_y (mtaz_net16_r3.hip; f16x3 variant 3): one stored-units exponent per workgroup
+void launch_net_f16x3_r3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
+                         float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
+                         int variant);
 // diagnostic instantiation with per-phase s_memtime stamps (never the product path)
 void launch_net_f16x3_stamped(const Dev& d, const NetWeights& w, const Pos* pos, int n, float* logits_out,
                               float* values_out, unsigned long long* stamps, hipStream_t s, int variant);

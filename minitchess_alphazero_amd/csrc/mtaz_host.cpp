@@ -1139,6 +1139,15 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
             }
           }
   }
+  // round 4's k_net_y: wy k-block-major (NetWeights::convyk)
+  std::vector<_Float16> wk(wy.size());
+  for (int L = 0; L < CONV_LAYERS; ++L) {
+    const _Float16* src = wy.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    _Float16* dst = wk.data() + (size_t)L * CONVX_U4_PER_LAYER * 8;
+    for (int ct = 0; ct < 16; ++ct)
+      for (int kb = 0; kb < 72; ++kb)
+        memcpy(dst + ((size_t)kb * 16 + ct) * 2 * 64 * 8, src + ((size_t)ct * 72 + kb) * 2 * 64 * 8, 2 * 64 * 8 * 2);
+  }
   // k_net_z's row-interleaved copies of wy and sy (NetWeights::convz, stemz)
   std::vector<_Float16> wz(wy.size()), sz(sy.size());
   for (int L = 0; L < CONV_LAYERS; ++L) {
@@ -1195,9 +1204,9 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.yrange = h->wyrange;
   const size_t nx = wy.size() / 8, nsy = sy.size() / 8, n8 = w8.size() / 16;
   const size_t nsc = (sc8.size() + 3) / 4, n6 = w6.size() / 16;
-  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6 | convz | stemz
+  // device layout (16-B units): convy | stemy | conv8 | conv8_sc | conv6 | convz | stemz | convyk
   const size_t o_sy = nx, o_w8 = o_sy + nsy, o_sc = o_w8 + n8, o_w6 = o_sc + nsc, o_wz = o_w6 + n6;
-  const size_t o_sz = o_wz + nx, o_end = o_sz + nsy;
+  const size_t o_sz = o_wz + nx, o_wk = o_sz + nsy, o_end = o_wk + nx;
   if (!h->wxbuf) ECHK(h->dalloc(&h->wxbuf, o_end));
   if (!h->wxinv) ECHK(h->dalloc(&h->wxinv, CONV_LAYERS + 1));
   HIPCHK(hipMemcpy(h->wxbuf, wy.data(), nx * 16, hipMemcpyHostToDevice));
@@ -1207,6 +1216,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   HIPCHK(hipMemcpy(h->wxbuf + o_w6, w6.data(), n6 * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_wz, wz.data(), nx * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxbuf + o_sz, sz.data(), nsy * 16, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->wxbuf + o_wk, wk.data(), nx * 16, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->wxinv, winv.data(), (CONV_LAYERS + 1) * 4, hipMemcpyHostToDevice));
   h->w.convx_inv = h->wxinv;
   h->w.stemx_inv = h->wxinv + CONV_LAYERS;
@@ -1217,6 +1227,7 @@ extern "C" int mtaz_set_weights(mtaz_engine* h, const float* const* d_tensors, c
   h->w.conv6 = h->wxbuf + o_w6;
   h->w.convz = h->wxbuf + o_wz;
   h->w.stemz = h->wxbuf + o_sz;
+  h->w.convyk = h->wxbuf + o_wk;
   h->weights_ok = true;
   ECHK(clear_batch_memo(h));   // results of the previous network
   return 0;
@@ -1282,7 +1293,9 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
 }
 
 // Variants a product library accepts: each parity-green against the reference fixtures
-// (tests/test_gpu_net.py).  k_net_y: 1024 = unfused epilogue (bit-identity reference).  k_net_z:
+// (tests/test_gpu_net.py).  k_net_y: 1 = 4 boards per workgroup in every round (no tail launch),
+// 2 = the class tiles without the tap skip (bit-identity reference of the skip), 3 = round 3's
+// kernel (k_net_y3, mtaz_net16_r3.hip: bit-identity reference below 2^14, A/B).  k_net_z:
 // 1 = the product kernel with 4 boards per workgroup in every round (no tail launches; bit-identity
 // reference and A/B for the tail-balanced assignment), 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms,
 // 25165824 = the round-2 K loop (per-step fragment addresses, global-address weights; bit-identity
@@ -1300,7 +1313,7 @@ extern "C" int mtaz_diag_select_stamps(unsigned long long* out8, int reset) {
 
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
-  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 1024 || variant == 114688 || variant == 16777216;
+  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 2 || variant == 3;
   if (h->precision == NET_F16F8)
     ok = ok || variant == 1 || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 ||
          variant == 33554432 || variant == 8388608 + 16777216 + 33554432;

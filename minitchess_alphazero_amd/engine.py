@@ -105,14 +105,15 @@ class Engine:
     def set_net_variant(self, variant):
         """Select a parity-tested build of the current precision's network kernel (0 = product;
         set_precision resets it).  f16x3 (k_net_y): 1 = 4 boards per workgroup in every round (no
-        tail launches), 1024 = the epilogue in unfused form, 114688 = the K loop without the LDS
-        offset table, buffer loads and 2-slot weight ring; all bitwise equal to 0.  f16f8
-        (k_net_z): 1 = 4 boards per workgroup in every round (no tail launches), 2097152 = the
-        epilogue in unfused form, 8192 = e2m3 (fp6) cross terms,
-        25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),
+        tail launch), 2 = the class tiles without the off-board tap skip, both bitwise equal to 0;
+        3 = round 3's kernel (one stored-units exponent per workgroup; bitwise equal to 0 on nets
+        whose activations stay below 2^14).  f16f8 (k_net_z): 1 = 4 boards per workgroup in every
+        round (no tail launches), 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross
+        terms, 25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),
         33554432 = the round-2 epilogue (unscaled conversions), 58720256 = both (the round-2
-        product); all but 8192 bitwise equal to 0.  Other values are rejected; the A/B and timing-only diagnostic builds exist only in
-        libmtaz_diag.so (MTAZ_LIB, tools/bench_net.py --diag)."""
+        product); all but 8192 bitwise equal to 0.  Other values are rejected; the A/B and
+        timing-only diagnostic builds exist only in libmtaz_diag.so (MTAZ_LIB, tools/bench_net.py
+        --diag)."""
         _lib.check(self.L.mtaz_set_net_variant(self.h, int(variant)))
 
     def set_pipeline(self, groups):

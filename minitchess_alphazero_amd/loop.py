@@ -89,10 +89,13 @@ def arena_round(new_net, old_net, games, sims, dist, device, seed_base):
 
 
 def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None, device=0, seed=0,
-             log=print, arena_games=0, gate_threshold=0.55, on_iteration=None):
+             log=print, arena_games=0, gate_threshold=0.55, on_iteration=None, starts=None):
     """C5 on this node.  Returns rank 0's per-iteration history (other ranks: []).
     on_iteration(it, net, records, history_entry), rank 0 only, after the weights of
-    iteration `it` are in place (tools/train_stress.py measures the network there)."""
+    iteration `it` are in place (tools/train_stress.py measures the network there).
+    starts(it, rank, games) -> None (every game from STARTING_FEN, the reference's puppet) or a list
+    of `games` FENs to start this iteration's games from (tools/train_stress.py mixes endgame
+    starts in, so that the value targets are not all draws)."""
     from .engine import Engine
     rank = dist.get_rank() if dist is not None else 0
     world = dist.get_world_size() if dist is not None else 1
@@ -109,7 +112,12 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
     for it in range(iterations):
         t0 = time.perf_counter()
         eng.set_seed_base((it * world + rank) * games)
-        st = eng.play()
+        fens = starts(it, rank, games) if starts is not None else None
+        if fens is None:
+            st = eng.play()
+        else:
+            eng.set_games(fens)
+            st = eng.play(from_current=True)
         rec = EpisodeRecords.from_engine(eng.records())
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
@@ -148,7 +156,7 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
                  'weights_version': out['version'], 'selfplay_s': t1 - t0, 'gather_s': t2 - t1,
                  'train_s': t3 - t2, 'broadcast_s': t4 - t3, 'iteration_s': t4 - t0,
                  'games_per_s': games * world / (t4 - t0), 'samples_per_s_train': rows / (t3 - t2),
-                 'plies_per_game': st['plies'] / games}
+                 'plies_per_game': st['plies'] / games, 'decisive_frac': st['decisive'] / games}
             if verdict is not None:
                 h['arena'] = verdict
             if on_iteration is not None:

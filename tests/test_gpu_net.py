@@ -88,25 +88,30 @@ def test_net_vs_torch_cpu_many_positions(engine):
     assert worst <= LOGIT_TOL
 
 
-def test_mix_epilogue_bit_identical():
-    """k_net_y's product epilogue (v_fma_mix forms) stores exactly the bits of the unfused
-    expressions (variant 1024): logits and values of the two builds must be bitwise equal."""
+def test_y_bit_identical_to_round3():
+    """Round 4's k_net_y (class tiles with the off-board taps skipped, one stored-units exponent per
+    board) computes exactly round 3's k_net_y (variant 3) on nets whose activations stay below 2^14
+    (both keep xs = 0 there): logits and values bitwise equal, main and tail launches alike."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from minitchess_alphazero_amd.network import Network
     from tests_positions import random_fens
     import torch
-    eng = Engine(n_games=64, sims=8)
-    eng.set_precision('f16x3')
     torch.manual_seed(0)
-    eng.set_weights(Network())
-    pos = np.stack([pos_from_fen(f) for f in random_fens(257, seed=5)])
-    eng.set_net_variant(0)
-    l0, v0 = eng.evaluate(pos)
-    eng.set_net_variant(1024)
-    l1, v1 = eng.evaluate(pos)
-    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
-    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+    fens = random_fens(400, seed=5)
+    for net in (Network(), _tiny_activation_net()):
+        eng = Engine(n_games=4096, sims=4)
+        eng.set_precision('f16x3')
+        eng.set_weights(net)
+        for n in (257, 1024 + 400, 2048 + 900):
+            pos = np.stack([pos_from_fen(fens[i % len(fens)]) for i in range(n)])
+            eng.set_net_variant(0)
+            l0, v0 = eng.evaluate(pos)
+            eng.set_net_variant(3)
+            l1, v1 = eng.evaluate(pos)
+            assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), n
+            assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), n
+        eng.close()
 
 
 def test_product_library_rejects_untested_variants():
@@ -117,8 +122,8 @@ def test_product_library_rejects_untested_variants():
     eng = Engine(n_games=4, sims=2)
     for prec, good, bad in (('f16f8', [0, 1, 8192, 2097152, 25165824, 33554432, 58720256],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
-                            ('f16x3', [0, 1, 1024, 114688, 16777216],
-                             [512, 4, 8, 2048, 8192, 4096, 268435456, 16384, 32768])):
+                            ('f16x3', [0, 1, 2, 3],
+                             [512, 4, 8, 1024, 114688, 16777216, 2048, 8192, 4096, 268435456, 16384, 32768])):
         eng.set_precision(prec)
         for v in good:
             eng.set_net_variant(v)
@@ -177,13 +182,10 @@ def test_z_loop_forms_bit_identical():
         assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
 
 
-def test_y_loop_forms_bit_identical():
-    """k_net_y's K loop with the LDS offset table, buffer-loaded weights and the 2-slot weight ring
-    (the product) computes exactly the loop before them (variant 114688), and the chunk-major LDS
-    image exactly the row-major swizzled one of rounds 1-3 (variant 16777216): logits and values
-    bitwise equal on an ordinary, a wide-range and a tiny-activation net.  1024 boards = one full
-    round of 4 boards per workgroup on 256 CUs, so the builds group the boards alike (the variants
-    have no tail launches)."""
+def test_y_tap_skip_bit_identical():
+    """Skipping the off-board taps (variant 0) changes no bit: the class-tiled kernel with every MFMA
+    run (variant 2) gives bitwise the same logits and values, on an ordinary, a wide-range (xs > 0)
+    and a tiny-activation net.  1024 boards = one full round of 4 boards per workgroup."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from minitchess_alphazero_amd.network import Network
@@ -197,28 +199,29 @@ def test_y_loop_forms_bit_identical():
         eng.set_weights(net)
         eng.set_net_variant(0)
         l0, v0 = eng.evaluate(pos)
-        for var in (114688, 16777216):
-            eng.set_net_variant(var)
-            l1, v1 = eng.evaluate(pos)
-            assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), var
-            assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), var
+        eng.set_net_variant(2)
+        l1, v1 = eng.evaluate(pos)
+        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
+        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+        eng.close()
 
 
-@pytest.mark.parametrize('precision', ['f16f8', 'f16x3'])
-@pytest.mark.parametrize('net_kind', ['seed0', 'tiny'])
+@pytest.mark.parametrize('precision,net_kind', [('f16f8', 'seed0'), ('f16f8', 'tiny'), ('f16x3', 'seed0'),
+                                               ('f16x3', 'tiny'), ('f16x3', 'wide'), ('f16x3', 'stress')])
 def test_tail_launches_bit_identical(net_kind, precision):
     """The tail-balanced board assignment (k_net_z, k_net_y: the boards beyond the full rounds of
     4 x CUs go to workgroups of 1, 2 or 3 boards) computes every board exactly as 4 boards per
     workgroup do (variant 1): batch sizes whose tails take each of the three tail builds and none.
-    (A net whose activations pass 2^14, like _wide_range_net, shares one stored-units exponent per
-    workgroup, so its boards can differ in the last bits with the grouping.)"""
+    k_net_y keeps one stored-units exponent per board, so this holds for nets whose activations
+    pass 2^14 too (wide, stress); k_net_z's is per workgroup (tested below 2^14 only)."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from minitchess_alphazero_amd.network import Network
     from tests_positions import random_fens
     import torch
     torch.manual_seed(0)
-    net = {'seed0': Network, 'wide': _wide_range_net, 'tiny': _tiny_activation_net}[net_kind]()
+    net = {'seed0': Network, 'wide': _wide_range_net, 'tiny': _tiny_activation_net,
+           'stress': _stress_net}[net_kind]()
     fens = random_fens(400, seed=29)
     eng = Engine(n_games=4096, sims=4)
     eng.set_precision(precision)
@@ -251,10 +254,11 @@ def _tiny_activation_net(scale=2.0 ** -20):
     return net.eval()
 
 
-@pytest.mark.parametrize('precision,var0,var1', [('f16f8', 0, 2097152), ('f16f8', 0, 33554432), ('f16x3', 0, 1024)])
+@pytest.mark.parametrize('precision,var0,var1', [('f16f8', 0, 2097152), ('f16f8', 0, 33554432), ('f16x3', 0, 3)])
 def test_mix_epilogue_bit_identical_tiny_activations(precision, var0, var1):
     """The v_fma_mix epilogues equal their unfused forms bitwise also when the activations are
-    f16-subnormal (the mix path's exactness precondition)."""
+    f16-subnormal (the mix path's exactness precondition); k_net_y equals round 3's
+    kernel (whose epilogue was pinned to its unfused form that way) on the same net."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from tests_positions import random_fens
@@ -322,22 +326,46 @@ def test_dynamic_range_beyond_f16(precision, var):
                 assert legal[int(np.argmax(logits[i][legal]))] == legal[int(np.argmax(p[i][legal]))]
 
 
-def test_dynamic_range_epilogue_bit_identical():
-    """With the image scale active (xs > 0), the v_fma_mix epilogue still stores exactly the
-    bits of the unfused form (variant 1024)."""
+def _stress_net():
+    """The round-3 stress checkpoint (tests/golden/stress/): trained in the C5 loop, trunk
+    activations in the thousands."""
+    from safetensors.torch import load_file
+    from minitchess_alphazero_amd.network import Network
+    net = Network()
+    net.load_state_dict(load_file(os.path.join(GOLDEN, 'stress', 'stress.safetensors')))
+    return net.eval()
+
+
+@pytest.mark.parametrize('net_kind', ['wide', 'stress'])
+def test_board_results_independent_of_batch(net_kind):
+    """a board's logits and value do not depend on the other boards of its batch or
+    workgroup (the reference evaluates every leaf batch-1, exp/agent.py:67-69), also once the
+    activations pass 2^14 and the stored-units exponent is nonzero.  The same positions in three
+    batch compositions (another order, interleaved with other positions, other batch sizes taking
+    other tail builds) give bitwise the same results per position."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from tests_positions import random_fens
-    eng = Engine(n_games=1024, sims=4)
+    net = {'wide': _wide_range_net, 'stress': _stress_net}[net_kind]()
+    fens = random_fens(1300, seed=41)
+    pos = np.stack([pos_from_fen(f) for f in fens])
+    eng = Engine(n_games=4096, sims=4)
     eng.set_precision('f16x3')
-    eng.set_weights(_wide_range_net())
-    # 1024 boards = one full round of 4 boards per workgroup on 256 CUs: both builds group the boards
-    # alike (the stored-units exponent is per workgroup, so a tail launch's regrouping may round
-    # differently once activations pass 2^14; test_tail_launches_bit_identical covers nets below)
-    pos = np.stack([pos_from_fen(f) for f in random_fens(1024, seed=4)])
-    eng.set_net_variant(0)
+    eng.set_weights(net)
     l0, v0 = eng.evaluate(pos)
-    eng.set_net_variant(1024)
-    l1, v1 = eng.evaluate(pos)
-    assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32))
-    assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(len(pos))
+    l1, v1 = eng.evaluate(pos[perm])
+    assert np.array_equal(l1.view(np.uint32), l0[perm].view(np.uint32))
+    assert np.array_equal(v1.view(np.uint32), v0[perm].view(np.uint32))
+    other = np.stack([pos_from_fen(f) for f in random_fens(1500, seed=43)])
+    mix = np.concatenate([other[:700], pos[:500], other[700:], pos[500:]])
+    l2, v2 = eng.evaluate(mix)
+    sel = np.r_[700:1200, 2000:2800]
+    assert np.array_equal(l2[sel].view(np.uint32), l0.view(np.uint32))
+    assert np.array_equal(v2[sel].view(np.uint32), v0.view(np.uint32))
+    for n in (37, 333, 1111):
+        l3, v3 = eng.evaluate(pos[:n])
+        assert np.array_equal(l3.view(np.uint32), l0[:n].view(np.uint32)), n
+        assert np.array_equal(v3.view(np.uint32), v0[:n].view(np.uint32)), n
+    eng.close()

@@ -31,9 +31,12 @@ run() {   # name timeout command...
   local name=$1 lim=$2
   shift 2
   echo "[gpu.sh] $name: $*" >&2
+  local t0=$(date +%s.%N)
   timeout -k 10 "$lim" "$@"
   local rc=$?
-  echo "[gpu.sh] $name rc=$rc" >&2
+  local t1=$(date +%s.%N)
+  echo "[gpu.sh] $name rc=$rc wall_s=$(awk "BEGIN{printf \"%.1f\", $t1 - $t0}")" >&2
+  echo "$name rc=$rc wall_s=$(awk "BEGIN{printf \"%.1f\", $t1 - $t0}")" >> "$OUT/walls.txt"
   return $rc
 }
 
@@ -63,14 +66,14 @@ for step in "$@"; do
                  "SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
         i=$((i + 1))
         run "pmc $i ($grp)" "${PMC_TIMEOUT:-420}" rocprofv3 --pmc $grp --kernel-include-regex "k_net_[yz]" \
-          -d "$OUT/pmc/p$i" -o pmc --output-format csv -- python3 bench.py ${PMC_ARGS:---no-cpu-baseline --no-secondary --default-sims 0} \
+          -d "$OUT/pmc/p$i" -o pmc --output-format csv -- python3 bench.py ${PMC_ARGS:---no-cpu-baseline --default-sims 0} \
           > "$OUT/pmc_p$i.log" 2>&1
         rc=$?; tail -1 "$OUT/pmc_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
     pmci)
       run pmci "${PMC_TIMEOUT:-420}" rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
         SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE --kernel-include-regex "k_net_[yz]" \
-        -d "$OUT/pmci" -o pmc --output-format csv -- python3 bench.py ${PMC_ARGS:---no-cpu-baseline --no-secondary --default-sims 0} \
+        -d "$OUT/pmci" -o pmc --output-format csv -- python3 bench.py ${PMC_ARGS:---no-cpu-baseline --default-sims 0} \
         > "$OUT/pmci.log" 2>&1
       rc=$?; tail -1 "$OUT/pmci.log"; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     ab|netab)
