@@ -153,6 +153,22 @@ __device__ __forceinline__ void ny_add4(f32x4v& m, const f32x4v& a) {
   m[2] = ny_add(m[2], a[2]);
   m[3] = ny_add(m[3], a[3]);
 }
+// wave-wide max of unsigned v, in lane 63: DPP steps (quad permutes, half-row and row mirrors, row
+// broadcasts 15 / 31) instead of six dependent ds_bpermute round trips
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xb1, 0xf, 0xf, false));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4e, 0xf, 0xf, false));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xf, 0xf, false));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xf, 0xf, false));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));
+  v = __builtin_elementwise_max(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+// ReLU on the float's bits (signed integer max with 0): negative values and -0 give +0, no
+// canonicalisation; a NaN stays a NaN (and reaches the overflow check)
+__device__ __forceinline__ float relu_bits(float x) {
+  return __int_as_float(__builtin_elementwise_max(__float_as_int(x), 0));
+}
 template <class T>
 __device__ __forceinline__ T sel4(int b, T x0, T x1, T x2, T x3) {
   return b == 0 ? x0 : b == 1 ? x1 : b == 2 ? x2 : x3;
@@ -240,18 +256,20 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
     // the lane's tile map is re-read here, so that its per-tile cell addresses are computed in the
     // epilogue instead of hoisted out of the layer loop into spilled registers
     asm volatile("" : "+v"(bp_lo), "+v"(bp_hi));
+    // board b's exponents, packed 8 bits per board (biased by 128) so that a lane picks its board's
+    // with one bit-field extract (no per-lane branch): dx = xs - xo (input and residual scale),
+    // dn = -xo (bias scale)
     int xo[4];
-    float insc[4], stv[4], ssd[4];
+    uint32_t pdx = 0, pdn = 0;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       xo[b] = bound[b] >= 16384.f ? (int)((__float_as_uint(bound[b]) >> 23) & 0xffu) - 127 - 14 : 0;
-      insc[b] = __builtin_ldexpf(inv, xs[b] - xo[b]);
-      stv[b] = __builtin_ldexpf(1.f, -xo[b]);
-      ssd[b] = __builtin_ldexpf(s_next, xs[b] - xo[b]);
+      pdx |= (uint32_t)(xs[b] - xo[b] + 128) << (8 * b);
+      pdn |= (uint32_t)(128 - xo[b]) << (8 * b);
     }
-    float ymt[8];
+    uint32_t ymt[8];   // per tile: the max of the lane's real square (float bits; y >= 0)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) ymt[t] = 0.f;
+    for (int t = 0; t < 8; ++t) ymt[t] = 0u;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int co0 = 16 * CT * wave + 16 * ct + 4 * g;
@@ -260,9 +278,9 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
       for (int t = 0; t < 8; ++t) {
         if ((t & 3) >= NVB) continue;
         const int v = bp_of(t), b = v & 3, p = v >> 2;
-        const float is = sel4(b, insc[0], insc[1], insc[2], insc[3]);
-        const float sv = sel4(b, stv[0], stv[1], stv[2], stv[3]);
-        const float sd = sel4(b, ssd[0], ssd[1], ssd[2], ssd[3]);
+        const int dx = (int)__builtin_amdgcn_ubfe(pdx, 8 * b, 8) - 128;
+        const int dn = (int)__builtin_amdgcn_ubfe(pdn, 8 * b, 8) - 128;
+        const float is = __builtin_ldexpf(inv, dx), sv = __builtin_ldexpf(1.f, dn);
         f32x4v& acc_t = acc[ct * 8 + t];
         f32x4v& a = mst[ct * 8 + t];
         if (t >= 4) {   // half-1 tiles: the last chunk's sums are still pending
@@ -270,15 +288,19 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
           acc_t = (f32x4v){0};
         }
         float y[4];
-        y[0] = fmaxf(__builtin_fmaf(a[0], is, bu.x * sv), 0.f);
-        y[1] = fmaxf(__builtin_fmaf(a[1], is, bu.y * sv), 0.f);
-        y[2] = fmaxf(__builtin_fmaf(a[2], is, bu.z * sv), 0.f);
-        y[3] = fmaxf(__builtin_fmaf(a[3], is, bu.w * sv), 0.f);
+        y[0] = relu_bits(__builtin_fmaf(a[0], is, bu.x * sv));
+        y[1] = relu_bits(__builtin_fmaf(a[1], is, bu.y * sv));
+        y[2] = relu_bits(__builtin_fmaf(a[2], is, bu.z * sv));
+        y[3] = relu_bits(__builtin_fmaf(a[3], is, bu.w * sv));
         // padding squares 30, 31 are computed and stored like the others (never a fragment source
-        // of a real square, never read by the heads) and stay out of the max
-        if (p < 30) ymt[t] = fmaxf(ymt[t], fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
+        // of a real square, never read by the heads) and stay out of the max (masked, no branch)
+        const uint32_t ym = __builtin_elementwise_max(
+            __builtin_elementwise_max(__float_as_uint(y[0]), __float_as_uint(y[1])),
+            __builtin_elementwise_max(__float_as_uint(y[2]), __float_as_uint(y[3])));
+        ymt[t] = __builtin_elementwise_max(ymt[t], ym & (0u - (uint32_t)(p < 30)));
         const int ah = cell(b, p) + 256 * (co0 >> 3) + 8 * (g & 1), al = ah + PART_B;
         if constexpr (conv_a) {
+          const float sd = __builtin_ldexpf(s_next, dx);
           const uint2 xh = *reinterpret_cast<const uint2*>(smem + ah);
           const uint2 xl = *reinterpret_cast<const uint2*>(smem + al);
           a[0] = ny_mix_lo(xh.x, sd, ny_mix_lo(xl.x, sd, 0.f));
@@ -296,21 +318,20 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         *reinterpret_cast<uint2*>(smem + al) = make_uint2(ny_lo_pair(hp.x, y[0], y[1]), ny_lo_pair(hp.y, y[2], y[3]));
       }
     }
-    // per-board max of the new image (y >= 0: float bits order as values; NaN above +inf)
-    float ymb[4] = {0.f, 0.f, 0.f, 0.f};
+    // per-board max of the new image (y >= 0: float bits order as values; NaN above +inf), each
+    // tile's max masked into its board's
+    uint32_t ymb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       if ((t & 3) >= NVB) continue;
       const int b = bp_of(t) & 3;
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) ymb[bb] = b == bb ? fmaxf(ymb[bb], ymt[t]) : ymb[bb];
+      for (int bb = 0; bb < 4; ++bb) ymb[bb] = __builtin_elementwise_max(ymb[bb], ymt[t] & (0u - (uint32_t)(b == bb)));
     }
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
-      float m = ymb[bb];
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      if (lane == 0) atomicMax(&mxs[4 * slot + bb], __float_as_uint(m));
+      const uint32_t m = wave_max_u32(ymb[bb]);
+      if (lane == 63) atomicMax(&mxs[4 * slot + bb], m);
     }
     if (tid < 4) mxs[4 * (slot ^ 1) + tid] = 0u;   // every wave read it before this epilogue's first barrier
 #pragma unroll
@@ -332,8 +353,8 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   }
   for (int i = tid; i < 2 * XB * IROWS; i += NT) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
   {   // the fragment offset table [tap 9][half 2][lane 64][tile i 4]: the byte offset of chunk g of
-      // the source square's cell | 1 on the board, the zero-line cell (bit 0 clear) off it; at the
-      // centre tap a padding square reads its own cell (its outputs are never used)
+      // the source square's cell | 1 on the board, the zero-line cell (bit 0 clear) off it and for
+      // the padding squares
     int* tab = reinterpret_cast<int*>(smem + IMG_B + AUXB);
     for (int e = tid; e < 9 * 2 * 64 * 4; e += NT) {
       const int i = e & 3, ln = (e >> 2) & 63, h = (e >> 8) & 1, tap = e >> 9;
@@ -429,7 +450,8 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   // row-gated tile (T in half 0, B in half 1) runs last, behind one uniform branch.
   const int tab_l = IMG_B + AUXB + 16 * lane;
   f16x8 A[2][2 * CT], BH[2][8];
-  uint4 tpre;
+  uint4 tpre;     // table entries of the half-step after next (read during the current one)
+  int onx[4];     // fragment offsets of the next half-step (computed at the end of the previous one)
   // weights k-block-major (NetWeights::convyk): the wave's fragment (channel tile ct, part) of
   // k-block kb at 32768 kb + 8192 wave + 2048 ct + 1024 part: the lane offset and the tile-pair's
   // 4 KB step in the scalar offset, the rest an immediate
@@ -447,7 +469,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
     o[3] = ny_mad_i24((int)(e.w & 1u), 1024 * kk7 - 1, (int)e.w);
   };
   for (int L = 0; L < CONV_LAYERS; ++L) {
-    // layer prologue: k-block 0's weights, half-step (0, 0)'s fragments, the table of (0, 1)
+    // layer prologue: k-block 0's weights, half-step (0, 0)'s fragments, the offsets of (0, 1)
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
       wload(A[0][2 * c], 0, c, 0);
@@ -455,6 +477,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
     }
     {
       const uint4 e0 = *reinterpret_cast<const uint4*>(smem + tab_l);
+      const uint4 e1 = *reinterpret_cast<const uint4*>(smem + tab_l + 1024);
       int o[4];
       offs(e0, 0, o);
 #pragma unroll
@@ -463,10 +486,9 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
           BH[0][i] = *reinterpret_cast<const f16x8*>(smem + o[i]);
           BH[0][4 + i] = *reinterpret_cast<const f16x8*>(smem + o[i] + PART_B);
         }
-      tpre = *reinterpret_cast<const uint4*>(smem + tab_l + 1024);
+      offs(e1, 0, onx);
     }
-    for (int j = 0; j < 3; ++j) {
-      const bool tact = j != 0, bact = j != 2;   // T: no dr = -1 taps; B: no dr = +1 taps
+    for (int j = 0; j < 3; ++j) {   // T (half 0) runs no dr = -1 taps (j = 0), B (half 1) no dr = +1 (j = 2)
       const int tab_j = tab_l + 6144 * j;
       const int tab_n = j < 2 ? tab_j + 6144 : tab_j;   // the next row's table (clamped in-bounds)
       const int kb_j = 24 * j;
@@ -505,8 +527,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
             for (int ct = 0; ct < CT; ++ct) acc[ct * 8 + 7] = (f32x4v){0};
           }
         }
-        int o[4];
-        offs(tpre, U1 & 7, o);
+        int o[4] = {onx[0], onx[1], onx[2], onx[3]};
         f16x8 (&BC)[8] = BH[H];
         f16x8 (&BN)[8] = BH[H1];
         f16x8 (&AC)[2 * CT] = A[U & 1];
@@ -562,7 +583,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         if constexpr (gated(NVB, SKIP, 4 * H + 3)) {
           constexpr int i = 3, t = 4 * H + i;
           constexpr bool fu = U == 0 || U == 12;
-          if (H ? bact : tact) {
+          if (j != (H ? 2 : 0)) {
             sfor<0, 12>([&](auto m_c) __attribute__((always_inline)) {
               constexpr int M = decltype(m_c)::value, ps = M / 4, ct = M % 4;
               acc[ct * 8 + t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AC[2 * ct + (ps == 2)], BC[(ps == 1) * 4 + i],
@@ -571,6 +592,9 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        // the offsets of the half-step after next (U2, H2), behind this half-step's last MFMAs, so
+        // that the next half-step issues its fragment reads at once
+        offs(tpre, U2 & 7, onx);
       });
     }
     stamp(st_k);

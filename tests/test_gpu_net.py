@@ -369,3 +369,36 @@ def test_board_results_independent_of_batch(net_kind):
         assert np.array_equal(l3.view(np.uint32), l0[:n].view(np.uint32)), n
         assert np.array_equal(v3.view(np.uint32), v0[:n].view(np.uint32)), n
     eng.close()
+
+
+@pytest.mark.parametrize('net_kind', ['wide', 'stress'])
+def test_round3_kernel_was_batch_dependent(net_kind):
+    """The case test_board_results_independent_of_batch guards against, shown on round 3's kernel
+    (variant 3, one stored-units exponent per workgroup): on these nets the exponent leaves 0, and
+    regrouping the same positions changes some boards' bits there, while round 4's per-board
+    exponent (variant 0) changes none.  Records how many positions differ."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from tests_positions import random_fens
+    from conftest import REPO
+    net = {'wide': _wide_range_net, 'stress': _stress_net}[net_kind]()
+    pos = np.stack([pos_from_fen(f) for f in random_fens(1300, seed=41)])
+    perm = np.random.default_rng(3).permutation(len(pos))
+    eng = Engine(n_games=4096, sims=4)
+    eng.set_precision('f16x3')
+    eng.set_weights(net)
+    diff = {}
+    for var in (3, 0):
+        eng.set_net_variant(var)
+        l0, v0 = eng.evaluate(pos)
+        l1, v1 = eng.evaluate(pos[perm])
+        same = (l1.view(np.uint32) == l0[perm].view(np.uint32)).all(axis=1) & (v1.view(np.uint32) == v0[perm].view(np.uint32))
+        diff[var] = int((~same).sum())
+    msg = f'{net_kind}: positions whose bits change with the batch order: round 3 {diff[3]}, round 4 {diff[0]}'
+    print(msg)
+    os.makedirs(os.path.join(REPO, 'gpurun_out'), exist_ok=True)
+    with open(os.path.join(REPO, 'gpurun_out', f'batch_dependence_{net_kind}.txt'), 'w') as fh:
+        fh.write(msg + '\n')
+    assert diff[0] == 0
+    assert diff[3] > 0
+    eng.close()

@@ -191,6 +191,9 @@ def main():
                     help='round 4: fraction of each iteration\'s games started from random endgame starts '
                          '(endgame_fen) instead of STARTING_FEN')
     ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--fallback-best', action='store_true',
+                    help='if no iteration qualifies, save the one past the other criteria with the largest '
+                         'value_std')
     ap.add_argument('--save', default='')
     args = ap.parse_args()
     from minitchess_alphazero_amd.build import build
@@ -199,12 +202,14 @@ def main():
     dev = torch.device('cuda', 0)
     torch.use_deterministic_algorithms(False)
     summary, found, last_rec = [], {}, [None]
+    best = {}
 
     class Done(Exception):
         pass
 
     for lr in [float(x) for x in args.lrs.split(',')]:
         t0 = time.time()
+        best[lr] = (-1.0, -1, None)
         last = {}
 
         def on_it(it, net, rec, h):
@@ -213,9 +218,13 @@ def main():
             m.update({'lr': lr, 'iteration': it, 'loss': h['loss'], 'plies_per_game': h['plies_per_game'],
                       'elapsed_s': round(time.time() - t0, 1)})
             m['decisive_frac'] = h.get('decisive_frac')
-            m['qualifies'] = (it >= args.min_iteration and m['trunk_max'] >= args.min_trunk
-                              and m['spread_max'] >= args.min_spread and m['logit_absmax'] <= args.max_logit
-                              and m['value_std'] >= args.min_value_std)
+            base_ok = (it >= args.min_iteration and m['trunk_max'] >= args.min_trunk
+                       and m['spread_max'] >= args.min_spread and m['logit_absmax'] <= args.max_logit)
+            m['qualifies'] = base_ok and m['value_std'] >= args.min_value_std
+            # --fallback-best: the network past the other criteria with the largest value_std, kept in
+            # case no iteration reaches --min-value-std
+            if args.fallback_best and base_ok and m['value_std'] > best[lr][0]:
+                best[lr] = (m['value_std'], it, {k: v.detach().cpu().clone().contiguous() for k, v in net.state_dict().items()})
             last.clear()
             last.update(m)
             print(json.dumps(m), flush=True)
@@ -241,8 +250,14 @@ def main():
         if found:
             break
     pick = next(iter(found), None)
+    fallback = None
+    if pick is None and args.fallback_best:
+        lr_b = max(best, key=lambda k: best[k][0])
+        if best[lr_b][2] is not None:
+            pick, fallback = lr_b, {'lr': lr_b, 'iteration': best[lr_b][1], 'value_std': best[lr_b][0]}
+            found[pick] = best[lr_b][2]
     out = {'summary': summary, 'picked_lr': pick, 'iterations_max': args.iterations, 'games': args.games,
-           'sims': args.sims, 'endgame_frac': args.endgame_frac, 'seed': args.seed,
+           'sims': args.sims, 'endgame_frac': args.endgame_frac, 'seed': args.seed, 'fallback_pick': fallback,
            'criteria': {'min_iteration': args.min_iteration, 'min_trunk': args.min_trunk,
                         'min_spread': args.min_spread, 'max_logit': args.max_logit,
                         'min_value_std': args.min_value_std}}
