@@ -132,8 +132,9 @@ int mtaz_stats(mtaz_engine* h, double* out, int n);
 /* record per-wave network HIP events during mtaz_play (trunk span for fp32, the fused
  * network kernel for fp16x3) */
 int mtaz_set_timing(mtaz_engine* h, int on);
-/* network arithmetic: 2 = k_net_z, f16 Wh*Xh + e4m3 cross terms (default, within 1e-5 of fp32),
- * 1 = k_net_y, fp16x3 split MFMA (fp32-accurate to ~1e-8), 0 = fp32 MFMA */
+/* network arithmetic: 1 = k_net_y (default), fp16x3 split MFMA, within 1e-5 of the reference on
+ * every tested net; 2 = k_net_z, f16 Wh*Xh + e4m3 cross terms (within 1e-5 on the seed-0 and C3
+ * nets only); 0 = fp32 MFMA */
 int mtaz_set_precision(mtaz_engine* h, int precision);
 /* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
 int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
@@ -181,7 +182,10 @@ int mtaz_set_edge_capacity(mtaz_engine* h, int64_t per_tree, int64_t pool);
  *      SimpleAlphaZeroPolicy.get_distribution, exp/policy.py:115-122) --------------- */
 int mtaz_set_games(mtaz_engine* h, const uint32_t* roots, const int32_t* agents, const uint8_t* active, int n);
 int mtaz_get_games(mtaz_engine* h, uint32_t* roots, int32_t* agents, uint8_t* active, int32_t* outcome);
-/* MonteCarloInit.on_episode_begin -> agent.init_mcts() (exp/callbacks.py:61-62): tree = 2*game + agent */
+/* MonteCarloInit.on_episode_begin -> agent.init_mcts() (exp/callbacks.py:61-62): tree = 2*game + agent.
+ * trees == NULL clears every table and empties the shared edge pool; a partial list clears those
+ * tables but does not return the pool edges they had taken (the pool is reclaimed by the next
+ * clear of all tables, which mtaz_play does) */
 int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n);
 /* root legal count and "root not yet visited" per game (decides the Dirichlet draws) */
 int mtaz_move_begin(mtaz_engine* h, int32_t* root_k, int32_t* root_new);

@@ -1383,6 +1383,13 @@ static int ensure_batch_memo(mtaz_engine* h) {
   return 0;
 }
 
+// frees the batch memo (play_groups: the groups' engines keep their own, sized for their games)
+static void release_batch_memo(mtaz_engine* h) {
+  for (void* p : h->memo_allocs) (void)hipFree(p);
+  h->memo_allocs.clear();
+  h->d.bm = BatchMemo{};
+}
+
 // empties the batch memo (new weights, new play)
 static int clear_batch_memo(mtaz_engine* h) {
   if (!h->d.bm.cap) return 0;
@@ -1713,7 +1720,11 @@ extern "C" int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* po
   std::vector<NodeHdr> hd(n);
   std::vector<uint32_t> hash(T.HC, 0u);
   const uint32_t ebase = (uint32_t)tree * (uint32_t)T.EC;
-  int64_t ne = 0;
+  // edges go to the table's own region while whole nodes fit there, the rest (from the first node
+  // that does not fit on) to one block of the shared pool, as k_select spills
+  int64_t ne = 0, nreg = 0;
+  bool spill = false;
+  std::vector<int64_t> off(n, 0);
   for (int i = 0; i < n; ++i) {
     np[i] = pos_in(pos + 5 * i);
     uint32_t s = pos_hash(np[i]) & (uint32_t)(T.HC - 1);
@@ -1725,10 +1736,26 @@ extern "C" int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* po
     }
     uint64_t sum = 0;
     for (int c = 0; c < k[i]; ++c) sum += N[e0[i] + c];
-    hd[i] = NodeHdr{ebase + (uint32_t)ne, (uint32_t)sum, (uint32_t)k[i], (float)tval[i]};
+    if (!spill && nreg + k[i] > T.EC) spill = true;
+    off[i] = ne;
+    if (!spill) nreg += k[i];
+    hd[i] = NodeHdr{0u, (uint32_t)sum, (uint32_t)k[i], (float)tval[i]};
     ne += k[i];
   }
-  if (ne > T.EC) return set_err(MTAZ_E_CAPACITY, "%lld edges do not fit a table region of %d", (long long)ne, T.EC);
+  const int64_t npool = ne - nreg;
+  uint32_t q = 0;
+  if (npool > 0) {   // one block of the pool (the stream is idle between moves: plain copies suffice)
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(&q, T.pool_used, 4, hipMemcpyDeviceToHost));
+    if ((uint64_t)q + (uint64_t)npool > (uint64_t)T.pool_cap)
+      return set_err(MTAZ_E_CAPACITY, "%lld edges beyond the table region do not fit the edge pool (%u of %u used)",
+                     (long long)npool, q, T.pool_cap);
+    const uint32_t q2 = q + (uint32_t)npool;
+    HIPCHK(hipMemcpy(T.pool_used, &q2, 4, hipMemcpyHostToDevice));
+  }
+  for (int i = 0; i < n; ++i)
+    if (!term[i])
+      hd[i].e0 = off[i] < nreg ? ebase + (uint32_t)off[i] : T.pool_base + q + (uint32_t)(off[i] - nreg);
   std::vector<uint16_t> ec(ne);
   std::vector<float> ep(ne);
   std::vector<double> eq(ne);
@@ -1742,18 +1769,22 @@ extern "C" int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* po
       en[o] = N[e0[i] + c];
     }
   }
-  const uint32_t nn32 = (uint32_t)n, ne32 = (uint32_t)ne;
+  const uint32_t nn32 = (uint32_t)n, ne32 = (uint32_t)nreg;
   HIPCHK(hipMemcpy(T.node_pos + (size_t)tree * T.NC, np.data(), n * sizeof(Pos), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(T.node_hdr + (size_t)tree * T.NC, hd.data(), n * sizeof(NodeHdr), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(T.hash + (size_t)tree * T.HC, hash.data(), (size_t)T.HC * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(T.n_nodes + tree, &nn32, 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(T.n_edges + tree, &ne32, 4, hipMemcpyHostToDevice));
-  if (ne) {
-    HIPCHK(hipMemcpy(T.e_code + ebase, ec.data(), ne * 2, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(T.e_P + ebase, ep.data(), ne * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(T.e_Q + ebase, eq.data(), ne * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(T.e_N + ebase, en.data(), ne * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(T.e_child + ebase, ech.data(), ne * 4, hipMemcpyHostToDevice));
+  // the region part at ebase, the pool part at pool_base + q
+  for (int part = 0; part < 2; ++part) {
+    const int64_t o = part ? nreg : 0, cnt = part ? npool : nreg;
+    if (cnt <= 0) continue;
+    const size_t d = part ? (size_t)T.pool_base + q : ebase;
+    HIPCHK(hipMemcpy(T.e_code + d, ec.data() + o, cnt * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_P + d, ep.data() + o, cnt * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_Q + d, eq.data() + o, cnt * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_N + d, en.data() + o, cnt * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(T.e_child + d, ech.data() + o, cnt * 4, hipMemcpyHostToDevice));
   }
   return 0;
 }
@@ -1783,6 +1814,7 @@ extern "C" int mtaz_set_timing(mtaz_engine* h, int on) {
 // back in game order, so the result equals the single-group run.
 static int play_groups(mtaz_engine* h) {
   const int ng = h->groups, Gp = h->G / ng;
+  release_batch_memo(h);   // idle while the groups play (up to 2^26 slots of 222 B); mtaz_play re-creates it
   if (h->parts.empty()) {
     for (int i = 0; i < ng; ++i) {
       mtaz_engine* p = mtaz_create(h->device, Gp, h->sims, h->cpuct, h->tau, h->alpha, h->eps, 0, h->cast_mode,
@@ -1851,6 +1883,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   }
   if (h->groups > 1 && !two_nets && !from_current && n_games == h->G) return play_groups(h);
   HIPCHK(hipSetDevice(h->device));
+  ECHK(ensure_batch_memo(h));   // (released while pipeline groups played)
   const double t0 = now_ms();
   const int G = h->G;
   for (int i = 0; i < ST_COUNT; ++i) h->stats[i] = 0;

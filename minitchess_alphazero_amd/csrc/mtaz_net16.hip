@@ -43,7 +43,7 @@ namespace ny {
 
 constexpr int KBY = 72;                     // k-blocks of 32 per conv
 constexpr int CELLS_B = 16384;              // per board and part: 32 squares x 32 chunks x 16 B
-constexpr int PART_B = CELLS_B + 512;       // + the zero line (32 cells of 16 B)
+constexpr int PART_B = CELLS_B + 512;       // + 512 B unused (round 3's zero line; keeps the heads' offset)
 constexpr int BOARD_B = 2 * PART_B;         // board b's parts hi, lo at b * BOARD_B (+ PART_B)
 constexpr int IMG_B = XB * BOARD_B;         // 135,168 B
 constexpr int TAB_B = 9 * 2 * 64 * 16;      // fragment offset table [tap][half][lane][4 tiles]
@@ -57,10 +57,20 @@ static_assert(SMEM_B <= 163840, "LDS");
 // by 4 per board.  A fragment read (each 16-lane LDS group = the 16 squares of one tile, any
 // chunk per lane) touches 16 distinct bank groups when the tile's 16 (board, square) pairs have
 // distinct (square + 4 board) mod 16, which the class tiles below are built to have (every tap
-// shifts all 16 by the same square offset; an off-board tap reads the board's zero-line cell on
-// the bank its source would have had).
+// shifts all 16 by the same square offset).  The padding squares 30, 31 of every board are kept
+// ZERO (the epilogue stores zeros there), so an off-board tap reads one of those 8 cells (4 boards
+// x 2 squares, bank groups 2, 3 mod 4) at the same chunk as an on-board tap: a lane's fragment
+// address is its table entry + 1024 (k-block mod 8), the step an immediate of the ds_read, with
+// no per-lane arithmetic.  The cell is chosen on the bank the source would have had when one is
+// (else that bank ^ 2): tools/net_tiles.py counts 12 extra LDS cycles over the 57 tile-taps.
 __device__ __forceinline__ int cell(int b, int r) { return b * BOARD_B + 8192 * (r >> 4) + 16 * ((r + 4 * b) & 15); }
-__device__ __forceinline__ int zcell(int b, int s) { return b * BOARD_B + CELLS_B + 16 * ((s + 4 * b) & 15); }
+// the zero cell (square 30 or 31 of some board) read in place of an off-board source whose cell
+// would have had bank group wb
+__device__ __forceinline__ int zcell(int wb) {
+  wb = (wb & 2) ? wb : wb ^ 2;
+  const int r = 30 + (wb & 1);
+  return cell(((wb - r) & 15) >> 2, r);
+}
 
 // The class tiles of a 4-board workgroup: lane n of tile t holds board (v & 3), square (v >> 2).
 // Half 0: tiles 0, 1 interior squares (rows 1-4, files 1-3), 2 = R (file 4, rows 1-4), 3 = T (top
@@ -114,12 +124,6 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 }  // namespace ny
 
-// a * b + c on v_mad_i32_i24 (b uniform; operands within 24 bits signed)
-__device__ __forceinline__ int ny_mad_i24(int a, int b, int c) {
-  int r;
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
-  return r;
-}
 // fma(f32(f16 half of pk), b, c) (v_fma_mix; exact in f32 where used, as round 3's)
 __device__ __forceinline__ float ny_mix_lo(uint32_t pk, float b, float c) {
   float r;
@@ -292,12 +296,17 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         y[1] = relu_bits(__builtin_fmaf(a[1], is, bu.y * sv));
         y[2] = relu_bits(__builtin_fmaf(a[2], is, bu.z * sv));
         y[3] = relu_bits(__builtin_fmaf(a[3], is, bu.w * sv));
-        // padding squares 30, 31 are computed and stored like the others (never a fragment source
-        // of a real square, never read by the heads) and stay out of the max (masked, no branch)
+        // the padding squares 30, 31 (tile X; the tail instances' half-1 tiles) store zeros: they
+        // are the zero cells of the off-board taps (masked, no branch)
+        if (NVB == XB ? t == 6 : t >= 4) {
+          const int keep = -(int)(p < 30);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) y[j] = __int_as_float(__float_as_int(y[j]) & keep);
+        }
         const uint32_t ym = __builtin_elementwise_max(
             __builtin_elementwise_max(__float_as_uint(y[0]), __float_as_uint(y[1])),
             __builtin_elementwise_max(__float_as_uint(y[2]), __float_as_uint(y[3])));
-        ymt[t] = __builtin_elementwise_max(ymt[t], ym & (0u - (uint32_t)(p < 30)));
+        ymt[t] = __builtin_elementwise_max(ymt[t], ym);
         const int ah = cell(b, p) + 256 * (co0 >> 3) + 8 * (g & 1), al = ah + PART_B;
         if constexpr (conv_a) {
           const float sd = __builtin_ldexpf(s_next, dx);
@@ -347,14 +356,14 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
 
   // ---------------- prologue: zero lines, stem input, fragment offset table ----------------
   char* simg = smem + IMG_B;
-  for (int i = tid; i < 2 * XB * 32; i += NT) {   // the zero lines
-    const int part = i / (XB * 32), bb = (i / 32) % XB, c = i & 31;
-    *reinterpret_cast<uint4*>(smem + bb * BOARD_B + part * PART_B + CELLS_B + 16 * c) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 2 * XB * 2 * 32; i += NT) {   // the padding squares 30, 31 (the zero cells)
+    const int q = i & 31, r = 30 + ((i >> 5) & 1), bb = (i >> 6) & 3, part = i >> 8;
+    *reinterpret_cast<uint4*>(smem + cell(bb, r) + 256 * q + part * PART_B) = make_uint4(0, 0, 0, 0);
   }
   for (int i = tid; i < 2 * XB * IROWS; i += NT) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
   {   // the fragment offset table [tap 9][half 2][lane 64][tile i 4]: the byte offset of chunk g of
-      // the source square's cell | 1 on the board, the zero-line cell (bit 0 clear) off it and for
-      // the padding squares
+      // the source square's cell on the board, of a zero cell (zcell) off it and for the padding
+      // squares
     int* tab = reinterpret_cast<int*>(smem + IMG_B + AUXB);
     for (int e = tid; e < 9 * 2 * 64 * 4; e += NT) {
       const int i = e & 3, ln = (e >> 2) & 63, h = (e >> 8) & 1, tap = e >> 9;
@@ -363,7 +372,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         const int v = tile_bp<NVB>(4 * h + i, ln & 15), b = v & 3, p = v >> 2, gg = ln >> 4;
         const int dh = tap / 3 - 1, dw = tap % 3 - 1, r = p / 5 + dh, c = p % 5 + dw, s = p + 5 * dh + dw;
         const bool valid = p < 30 && (unsigned)r < 6u && (unsigned)c < 5u;
-        ent = valid ? ((cell(b, s) + 256 * gg) | 1) : zcell(b, s);
+        ent = (valid ? cell(b, s) : zcell(s + 4 * b)) + 256 * gg;
       }
       tab[e] = ent;
     }
@@ -451,7 +460,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   const int tab_l = IMG_B + AUXB + 16 * lane;
   f16x8 A[2][2 * CT], BH[2][8];
   uint4 tpre;     // table entries of the half-step after next (read during the current one)
-  int onx[4];     // fragment offsets of the next half-step (computed at the end of the previous one)
+  int onx[4];     // table entries (fragment bases, k-block step aside) of the next half-step
   // weights k-block-major (NetWeights::convyk): the wave's fragment (channel tile ct, part) of
   // k-block kb at 32768 kb + 8192 wave + 2048 ct + 1024 part: the lane offset and the tile-pair's
   // 4 KB step in the scalar offset, the rest an immediate
@@ -461,12 +470,6 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   auto wload = [&](f16x8& dst, int kb, int ct, int part) __attribute__((always_inline)) {
     dst = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rsy, voy + ((ct & 1) * 2 + part) * 1024,
                                                                            lofs + kb * 32768 + (ct >> 1) * 4096, 0));
-  };
-  auto offs = [&](const uint4& e, int kk7, int* o) __attribute__((always_inline)) {
-    o[0] = ny_mad_i24((int)(e.x & 1u), 1024 * kk7 - 1, (int)e.x);
-    o[1] = ny_mad_i24((int)(e.y & 1u), 1024 * kk7 - 1, (int)e.y);
-    o[2] = ny_mad_i24((int)(e.z & 1u), 1024 * kk7 - 1, (int)e.z);
-    o[3] = ny_mad_i24((int)(e.w & 1u), 1024 * kk7 - 1, (int)e.w);
   };
   for (int L = 0; L < CONV_LAYERS; ++L) {
     // layer prologue: k-block 0's weights, half-step (0, 0)'s fragments, the offsets of (0, 1)
@@ -478,15 +481,14 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
     {
       const uint4 e0 = *reinterpret_cast<const uint4*>(smem + tab_l);
       const uint4 e1 = *reinterpret_cast<const uint4*>(smem + tab_l + 1024);
-      int o[4];
-      offs(e0, 0, o);
+      const int o[4] = {(int)e0.x, (int)e0.y, (int)e0.z, (int)e0.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (i < NVB) {
           BH[0][i] = *reinterpret_cast<const f16x8*>(smem + o[i]);
           BH[0][4 + i] = *reinterpret_cast<const f16x8*>(smem + o[i] + PART_B);
         }
-      offs(e1, 0, onx);
+      onx[0] = (int)e1.x, onx[1] = (int)e1.y, onx[2] = (int)e1.z, onx[3] = (int)e1.w;
     }
     for (int j = 0; j < 3; ++j) {   // T (half 0) runs no dr = -1 taps (j = 0), B (half 1) no dr = +1 (j = 2)
       const int tab_j = tab_l + 6144 * j;
@@ -548,7 +550,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
                   if (nd[i] && c++ == Q / 2) return i;
                 return 0;
               }();
-              BN[(Q & 1) * 4 + I] = *reinterpret_cast<const f16x8*>(smem + o[I] + (Q & 1) * PART_B);
+              BN[(Q & 1) * 4 + I] = *reinterpret_cast<const f16x8*>(smem + o[I] + 1024 * (U1 & 7) + (Q & 1) * PART_B);
             } else if constexpr (Q == NFR) {   // the table entries of (U2, H2)
               const int ta = U2 < 24 ? tab_j + (U2 / 8) * 2048 + H2 * 1024 : tab_n + ((U2 - 24) / 8) * 2048 + H2 * 1024;
               tpre = *reinterpret_cast<const uint4*>(smem + ta);
@@ -592,9 +594,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
           }
           __builtin_amdgcn_sched_barrier(0);
         }
-        // the offsets of the half-step after next (U2, H2), behind this half-step's last MFMAs, so
-        // that the next half-step issues its fragment reads at once
-        offs(tpre, U2 & 7, onx);
+        onx[0] = (int)tpre.x, onx[1] = (int)tpre.y, onx[2] = (int)tpre.z, onx[3] = (int)tpre.w;
       });
     }
     stamp(st_k);

@@ -58,8 +58,14 @@ def main():
     print(f'game_start: {len(g_start["moves"])} plies, reward {g_start["moves"][-1]["reward"]} '
           f'({time.time() - t0:.0f} s)', flush=True)
     g_end = None
-    for f in ends[:8]:
-        g = ref_selfplay(renv, rpol, ragent, rcb, net, 64, [0], start_fen=f)[0]
+    for f in ends[:32]:
+        try:
+            g = ref_selfplay(renv, rpol, ragent, rcb, net, 64, [0], start_fen=f)[0]
+        except renv.TerminatedEpisodeStepException:
+            # the reference's search steps a finished episode from some starts (exp/agent.py:86 on a
+            # position its environment calls over); such a start has no reference game
+            print(f'game_end from {f}: the reference raised TerminatedEpisodeStepException', flush=True)
+            continue
         print(f'game_end from {f}: {len(g["moves"])} plies, reward {g["moves"][-1]["reward"]}', flush=True)
         if g_end is None or (g['moves'][-1]['reward'] != 0 and g_end['moves'][-1]['reward'] == 0):
             g_end = g

@@ -122,10 +122,13 @@ def c3_network():
     return net.eval()
 
 
-def stress_network():
-    """The round-3 stress checkpoint (tools/train_stress.py, pinned by tests/golden/make_golden_r3.py):
-    21 reference-learner updates in the C5 loop at lr 0.02, trunk activations in the thousands,
-    legal-logit spreads up to ~80 on its fixture positions; sha256-checked."""
+def stress_network(name='stress'):
+    """A trained checkpoint of tests/golden/, sha256-checked against its pinned fixture json.
+    'stress' (round 3, tools/train_stress.py, pinned by make_golden_r3.py): 21 reference-learner
+    updates in the C5 loop at lr 0.02, trunk activations in the thousands, legal-logit spreads up
+    to ~80 on its fixture positions, its value head collapsed to a constant.  'stress4' (round 4,
+    pinned by make_golden_r4.py): 20 updates at lr 0.003 with half the games from endgame starts,
+    a value head whose outputs vary (-0.26 .. 0.33 on its fixture positions)."""
     import json
     import os
     from safetensors.torch import load_file
@@ -133,9 +136,9 @@ def stress_network():
     from oracle.net import state_dict_sha256
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
     net = Network()
-    net.load_state_dict(load_file(os.path.join(here, 'stress', 'stress.safetensors')))
-    meta = json.load(open(os.path.join(here, 'stress.json')))
-    assert state_dict_sha256(net) == meta['state_dict_sha256'], 'stress checkpoint does not match its pinned sha256'
+    net.load_state_dict(load_file(os.path.join(here, name, f'{name}.safetensors')))
+    meta = json.load(open(os.path.join(here, f'{name}.json')))
+    assert state_dict_sha256(net) == meta['state_dict_sha256'], f'{name} checkpoint does not match its pinned sha256'
     return net.eval()
 
 

@@ -130,3 +130,46 @@ def test_puppet_publishes_reference_payloads():
     p.remote_status = pp.MasterOfPuppetsStatus.TRAIN
     p.run_episodes(1, c)
     assert len(c.msgs) == 3
+
+
+def test_tree_set_spills_to_the_edge_pool():
+    """mtaz_tree_set places a table's edges like k_select does: in the table's own region while
+    whole nodes fit, the rest in the shared pool (it used to fail with E_CAPACITY beyond
+    the region).  A searched table moved into an engine whose per-table region is far too small
+    reads back identically and searches on exactly like the original."""
+    import torch
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import STARTING_FEN
+    from minitchess_alphazero_amd.network import Network
+    torch.manual_seed(0)
+    net = Network()
+    engs = []
+    for per_tree in (None, 24):
+        e = Engine(n_games=1, sims=64)
+        e.set_weights(net)
+        if per_tree:
+            e.set_edge_capacity(per_tree, 1 << 20)
+        e.set_games([STARTING_FEN])
+        e.clear_trees()
+        engs.append(e)
+    a, b = engs
+    k, new = a.move_begin()
+    rng = np.random.RandomState(1)
+    noise = [np.stack([rng.dirichlet([0.6] * int(k[0])) for _ in range(64 - int(new[0]))])]
+    a.set_noise(noise)
+    a.simulate(0, 40)
+    ta = a.tree_arrays(0)
+    assert int(ta['k'][:ta['n']].astype(np.int64).sum()) > 24     # more edges than b's region
+    b.set_tree(0, ta)
+    tb = b.tree_arrays(0)
+    for key in ('pos', 'e0', 'k', 'term', 'tval', 'codes', 'P', 'Q', 'N'):
+        assert np.array_equal(ta[key], tb[key]), key
+    kb, newb = b.move_begin()
+    assert int(kb[0]) == int(k[0]) and int(newb[0]) == 0      # b finds the root in the moved table
+    # simulation s reads draw s - root_new: a's draw s - 1 is b's draw s
+    b.set_noise([np.concatenate([noise[0][:1], noise[0]])])
+    a.simulate(40, 24)
+    b.simulate(40, 24)
+    ta, tb = a.tree_arrays(0), b.tree_arrays(0)
+    for key in ('pos', 'e0', 'k', 'term', 'tval', 'codes', 'P', 'Q', 'N'):
+        assert np.array_equal(ta[key], tb[key]), key

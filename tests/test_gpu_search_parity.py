@@ -24,6 +24,7 @@ import pytest
 
 from conftest import GOLDEN, REPO, load_golden
 from helpers import c3_network, compare_records, drive_engine, explain_divergence
+from minitchess_alphazero_amd.environment import STARTING_FEN
 
 pytestmark = pytest.mark.gpu
 
@@ -107,7 +108,9 @@ def _l3(name, precision, net, ref_net, games):
     eng.set_precision(precision)
     eng.set_weights(net)
     leaves = {}
-    recs, _ = drive_engine(eng, len(games), sims, [g['seed'] for g in games], evaluator=None, capture=leaves)
+    starts = [g.get('start') or STARTING_FEN for g in games]
+    recs, _ = drive_engine(eng, len(games), sims, [g['seed'] for g in games], evaluator=None, capture=leaves,
+                           start_fen=starts)
     rows = []
     for got, gm in zip(recs, games):
         same, total, first = compare_records(got, gm['moves'])

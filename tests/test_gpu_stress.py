@@ -21,8 +21,11 @@ the build container), with one 64-sim reference self-play game.
     precision is k_net_y (f16x3), and test_f16f8_outside_its_scope_on_the_stress_net records the
     measured deviation.
 The value head of this checkpoint has collapsed to a constant (-0.0117 on every position: the
-self-play data of the loop is almost all draws), so the value checks are weak here; the C3 net
-covers varying values."""
+self-play data of the loop is almost all draws), so the value checks are weak here.  Round 4's
+STRESS4 checkpoint (tools/train_stress.py --endgame-frac 0.5 --lrs 0.003, pinned by
+tests/golden/make_golden_r4.py) has a value head whose outputs vary (-0.26 .. 0.33, std 0.058 on
+its 191 fixture positions): the parity checks run on both, and on stress4 also its decisive
+reference game from an endgame start (L1, host leaves)."""
 import os
 
 import numpy as np
@@ -37,19 +40,22 @@ TOL = 1e-5
 EXACT = ['f16x3', 'fp32']          # the precisions whose north_star claim covers this net
 
 
-def _fixture():
-    z = np.load(os.path.join(GOLDEN, 'stress_net.npz'))
+CKPTS = ['stress', 'stress4']
+
+
+def _fixture(name='stress'):
+    z = np.load(os.path.join(GOLDEN, f'{name}_net.npz'))
     return [str(f) for f in z['fens']], z['logits'].astype(np.float64), z['values'].astype(np.float64)
 
 
-def _deviations(precision):
+def _deviations(precision, name='stress'):
     import torch
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen, pos_legal
-    fens, ref_l, ref_v = _fixture()
+    fens, ref_l, ref_v = _fixture(name)
     eng = Engine(n_games=len(fens), sims=4)
     eng.set_precision(precision)
-    eng.set_weights(stress_network())
+    eng.set_weights(stress_network(name))
     pos = np.stack([pos_from_fen(f) for f in fens])
     logits, values = eng.evaluate(pos)
     dl = float(np.max(np.abs(logits - ref_l) / np.maximum(1.0, np.abs(ref_l).max(axis=1, keepdims=True))))
@@ -73,10 +79,22 @@ def test_stress_checkpoint_pinned_and_stressed():
     assert meta['training']['summary']['criteria']['min_iteration'] >= 19     # >= 20 learner updates
 
 
+def test_stress4_checkpoint_pinned_and_values_vary():
+    """stress4's value head is not collapsed: its reference values on the fixture
+    positions span at least 0.4 with a standard deviation of at least 0.05."""
+    meta = load_golden('stress4')
+    stress_network('stress4')
+    _, _, ref_v = _fixture('stress4')
+    assert meta['training']['summary']['criteria']['min_iteration'] >= 19     # >= 20 learner updates
+    assert ref_v.max() - ref_v.min() >= 0.4 and ref_v.std() >= 0.05
+    assert meta['game_end']['moves'][-1]['reward'] != 0                       # a decisive reference game
+
+
+@pytest.mark.parametrize('name', CKPTS)
 @pytest.mark.parametrize('precision', EXACT)
-def test_stress_net_vs_reference(precision):
-    dl, dp, dv, dup = _deviations(precision)
-    print(f'stress {precision}: logits {dl:.3e} of the row scale, priors {dp:.3e}, values {dv:.3e}; '
+def test_stress_net_vs_reference(precision, name):
+    dl, dp, dv, dup = _deviations(precision, name)
+    print(f'{name} {precision}: logits {dl:.3e} of the row scale, priors {dp:.3e}, values {dv:.3e}; '
           f'{dup} legal lists with repeated codes')
     assert dl <= TOL and dp <= TOL and dv <= TOL
 
@@ -95,18 +113,19 @@ def test_f16f8_outside_its_scope_on_the_stress_net():
     assert Engine.DEFAULT_PRECISION == 'f16x3'
 
 
+@pytest.mark.parametrize('name', CKPTS)
 @pytest.mark.parametrize('precision', EXACT)
-def test_stress_leaf_priors_and_values(precision):
+def test_stress_leaf_priors_and_values(precision, name):
     """The priors and values the search consumes on this net (device-written leaf results of
     sim_evaluate) vs the reference's softmax over its own logits, repeated promotion codes kept."""
     import torch
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen, pos_legal, pos_outcome
-    fens, ref_l, ref_v = _fixture()
+    fens, ref_l, ref_v = _fixture(name)
     roots = [i for i, f in enumerate(fens) if pos_legal(pos_from_fen(f)) and pos_outcome(pos_from_fen(f)) == 0]
     eng = Engine(n_games=len(roots), sims=4)
     eng.set_precision(precision)
-    eng.set_weights(stress_network())
+    eng.set_weights(stress_network(name))
     eng.set_games([fens[i] for i in roots])
     eng.clear_trees()
     eng.move_begin()
@@ -122,7 +141,7 @@ def test_stress_leaf_priors_and_values(precision):
         ref = torch.from_numpy(ref_l[j][legal].astype(np.float32)).softmax(0).double().numpy()
         worst_p = max(worst_p, float(np.max(np.abs(P[i][:len(legal)].astype(np.float64) - ref))))
         worst_v = max(worst_v, abs(float(v[i]) - float(ref_v[j])))
-    print(f'stress leaves {precision}: {len(lgame)} leaves, max |P - ref| {worst_p:.3e}, max |v - ref| {worst_v:.3e}')
+    print(f'{name} leaves {precision}: {len(lgame)} leaves, max |P - ref| {worst_p:.3e}, max |v - ref| {worst_v:.3e}')
     assert worst_p <= TOL and worst_v <= TOL
     eng.sim_backup()
 
@@ -150,3 +169,31 @@ def test_stress_gpu_net_64_sims_vs_reference(precision):
     ref = RefNet()
     ref.load_state_dict(stress_network().state_dict())
     _l3('stress_64', precision, stress_network(), ref.eval(), [load_golden('stress')['stress_64']])
+
+
+@pytest.mark.parametrize('game', ['game_start', 'game_end'])
+def test_stress4_host_leaves_64_sims_equal_reference(game):
+    """L1 on stress4: the reference's 64-sim games (from STARTING_FEN, and the decisive one from an
+    endgame start), leaves evaluated batch-1 on the host exactly as exp/agent.py:66-69; every pi,
+    action and reward bit-exact."""
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import STARTING_FEN
+    from oracle.mcts import TorchNetEvaluator
+    from oracle.net import Network as RefNet
+    gm = load_golden('stress4')[game]
+    ref = RefNet()
+    ref.load_state_dict(stress_network('stress4').state_dict())
+    eng = Engine(n_games=1, sims=gm['sims'])
+    recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=TorchNetEvaluator(ref.eval()),
+                           start_fen=gm['start'] or STARTING_FEN)
+    assert compare_records(recs[0], gm['moves'])[2] is None
+    assert [x['reward'] for x in recs[0]] == [x['reward'] for x in gm['moves']]
+
+
+def test_stress4_gpu_net_64_sims_vs_reference():
+    """L3 on stress4 with the default network (k_net_y), the game from STARTING_FEN."""
+    from test_gpu_search_parity import _l3
+    from oracle.net import Network as RefNet
+    ref = RefNet()
+    ref.load_state_dict(stress_network('stress4').state_dict())
+    _l3('stress4_start', 'f16x3', stress_network('stress4'), ref.eval(), [load_golden('stress4')['game_start']])

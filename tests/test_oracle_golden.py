@@ -128,3 +128,26 @@ def test_terminal_revisit_quirk(golden):
                     assert seq[:3] == [1.0, 0.0, -1.0 / 3.0]
                     seen_quirk = True
         assert seen_quirk
+
+
+@pytest.mark.parametrize('name', ['stress', 'stress4'])
+def test_trained_checkpoint_outputs(name):
+    """The oracle's network (exp/policy.py restated) on the trained checkpoints reproduces the
+    reference's own outputs (make_golden_r3.py / make_golden_r4.py) on fixture positions: the
+    oracle the GPU parity tests compare against is pinned on these nets too, varying values
+    (stress4) included."""
+    import os
+    import torch
+    from safetensors.torch import load_file
+    from conftest import GOLDEN, load_golden
+    n = net.Network()
+    n.load_state_dict(load_file(os.path.join(GOLDEN, name, f'{name}.safetensors')))
+    n.eval()
+    assert net.state_dict_sha256(n) == load_golden(name)['state_dict_sha256']
+    z = np.load(os.path.join(GOLDEN, f'{name}_net.npz'))
+    idx = np.linspace(0, len(z['fens']) - 1, 12).astype(int)
+    with torch.no_grad():
+        for i in idx:
+            p, v = n(encoder.process_observation(str(z['fens'][i])))
+            assert np.max(np.abs(p[0].numpy() - z['logits'][i])) <= 1e-5 * max(1.0, float(np.abs(z['logits'][i]).max()))
+            assert abs(float(v.item()) - float(z['values'][i])) <= 1e-6

@@ -70,6 +70,18 @@ for step in "$@"; do
           > "$OUT/pmc_p$i.log" 2>&1
         rc=$?; tail -1 "$OUT/pmc_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
+    pmcnet)
+      # the network kernel alone (tools/bench_net.py, 4096 boards): one counter group per pass
+      i=0
+      for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+                 "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+                 "FETCH_SIZE TCC_HIT_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        i=$((i + 1))
+        run "pmcnet $i" "${PMC_TIMEOUT:-300}" rocprofv3 --pmc $grp --kernel-include-regex "k_net_y" \
+          -d "$OUT/pmcnet/p$i" -o pmc --output-format csv -- python3 tools/bench_net.py --variants ${PMCNET_VARIANTS:-f16x3:0} \
+          --rounds 1 --iters 5 > "$OUT/pmcnet_p$i.log" 2>&1
+        rc=$?; tail -1 "$OUT/pmcnet_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
+      done ;;
     pmci)
       run pmci "${PMC_TIMEOUT:-420}" rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
         SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE --kernel-include-regex "k_net_[yz]" \
