@@ -78,8 +78,8 @@ for step in "$@"; do
                  "FETCH_SIZE TCC_HIT_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
         i=$((i + 1))
         run "pmcnet $i" "${PMC_TIMEOUT:-300}" rocprofv3 --pmc $grp --kernel-include-regex "k_net_y" \
-          -d "$OUT/pmcnet/p$i" -o pmc --output-format csv -- python3 tools/bench_net.py --variants ${PMCNET_VARIANTS:-f16x3:0} \
-          --rounds 1 --iters 5 > "$OUT/pmcnet_p$i.log" 2>&1
+          -d "$OUT/pmcnet${PMCNET_TAG}/p$i" -o pmc --output-format csv -- python3 tools/bench_net.py --variants ${PMCNET_VARIANTS:-f16x3:0} \
+          --rounds 1 --iters 5 > "$OUT/pmcnet${PMCNET_TAG}_p$i.log" 2>&1
         rc=$?; tail -1 "$OUT/pmcnet_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
     pmci)
