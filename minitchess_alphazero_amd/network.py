@@ -4,9 +4,10 @@ Parameter creation order and state_dict keys equal the reference's
 (exp/policy.py:53-69), so `torch.manual_seed(0); Network()` yields the reference's
 random-init weights and `load_state_dict` accepts reference checkpoints.
 
-Self-play inference does not use this module's forward: it runs in the HIP kernels
-(k_net_z by default, csrc/mtaz_net8.hip; k_net_y, csrc/mtaz_net16.hip, with precision 'f16x3')
-through Engine.set_weights / Engine.evaluate.  The torch
+Self-play inference does not use this module's forward: it runs in the HIP kernels (k_net_y by
+default, csrc/mtaz_net16.hip, precision 'f16x3'; k_net_z, csrc/mtaz_net8.hip, precision 'f16f8',
+is an option outside the 1e-5 contract on trained nets) through Engine.set_weights /
+Engine.evaluate.  The torch
 forward below is the TRAINING path of the learner (exp/learner.py:84-88; autograd on
 PyTorch-ROCm): train-mode BatchNorm uses batch statistics, which the folded
 inference kernels cannot express.
