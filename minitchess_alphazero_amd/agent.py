@@ -104,16 +104,17 @@ class SimpleAlphaZeroAgent(PolicyAgent):
     counts while the fullmove number is below tau_change, else play a most-visited move
     (ties broken uniformly at random)."""
 
-    def __init__(self, environment, policy, num_simulations, cpuct=1, tau_change=6):
+    def __init__(self, environment, policy, num_simulations, cpuct=1, tau_change=6, device=0):
         super().__init__(policy)
         self._environment = environment
         self._num_simulations = num_simulations
         self._cpuct = cpuct
         self._tau_change = tau_change
+        self._device = device     # (not in the reference: the GPU the one-game engines run on)
         self.init_mcts()
 
     def init_mcts(self):
-        self._mcts = MonteCarloTreeSearch(self._environment, self.policy.model, self._cpuct)
+        self._mcts = MonteCarloTreeSearch(self._environment, self.policy.model, self._cpuct, device=self._device)
 
     def select_action(self, observation):
         dist = self.policy.get_distribution(observation, self._mcts, self._num_simulations)

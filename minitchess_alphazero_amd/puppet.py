@@ -15,9 +15,15 @@ records (minitchess_alphazero_amd.wire.episode_payloads), byte-identical to json
 Weights from rlweb: `load_weights_blob(body)` decodes the reference's download_weights body
 (zlib + json + jsonpickle, app/base.py:31-39) without unpickling (wire.load_weights_blob).
 
-RNG: the reference draws from the global np.random; here every game gets its own
-numpy-legacy stream seeded from one np.random.randint draw, so seeding np.random
-still makes a run reproducible.
+RNG: the reference plays its episodes one after another, every draw from the global np.random
+(app/base.py:113-120).  rng_stream='batched' (the default) plays them in parallel instead, every
+game on its own numpy-legacy stream seeded from one np.random.randint draw per batch, so seeding
+np.random still makes a run reproducible (game i of a batch plays as the reference does after
+np.random.seed(seed_base + i)).  rng_stream='global' keeps the reference's stream exactly: the
+episodes run in sequence through the drop-in agent stack (erlyx run_episodes + RoundRobinReferee +
+SimpleAlphaZeroAgent + InfoRecorder + MonteCarloInit, app/base.py:112-120 line for line), one game
+at a time on the GPU engine, so the payloads are those the reference publishes after the same
+np.random.seed (as fast as one game's search allows, not the batched throughput).
 
 Command line (no MQTT broker needed):
     python -m minitchess_alphazero_amd.puppet --episodes 64 --sims 36 --out episodes.jsonl
@@ -76,7 +82,11 @@ class MQTTDataset:
 
 
 class SimulatePuppet:
-    def __init__(self, userid, publish_topic, num_simulations=NUM_SIMULATIONS, device=0, max_parallel=4096):
+    def __init__(self, userid, publish_topic, num_simulations=NUM_SIMULATIONS, device=0, max_parallel=4096,
+                 rng_stream='batched'):
+        if rng_stream not in ('batched', 'global'):
+            raise ValueError(f"rng_stream must be 'batched' or 'global', not {rng_stream!r}")
+        self._rng_stream = rng_stream
         self._network = Network().eval()
         self._userid = userid
         self._publish_topic = publish_topic
@@ -166,6 +176,23 @@ class SimulatePuppet:
             yield from episode_payloads(eng.records(), self.userid, self.weights_version,
                                         MINITCHESS_ALPHAZERO_VERSION)[:n]
 
+    def _run_sequential(self, num_episodes, dataset):
+        """rng_stream='global': app/base.py:112-120 over the drop-in stack, episodes in sequence."""
+        import torch
+        from .agent import RoundRobinReferee, SimpleAlphaZeroAgent
+        from .callbacks import InfoRecorder, MonteCarloInit
+        from .environment import MinitChessEnvironment
+        from .erlyx_compat import run_episodes
+        from .policy import SimpleAlphaZeroPolicy
+        env = MinitChessEnvironment()
+        policy = SimpleAlphaZeroPolicy(network=self._network)
+        agents = [SimpleAlphaZeroAgent(environment=env, policy=policy, num_simulations=self._sims,
+                                       device=self._device) for _ in range(2)]
+        callbacks = [InfoRecorder(dataset), MonteCarloInit(agents[0]), MonteCarloInit(agents[1])]
+        with torch.no_grad():
+            run_episodes(env, RoundRobinReferee(agent_tuple=tuple(agents)), num_episodes, callbacks=callbacks,
+                         use_tqdm=False)
+
     def run_episodes(self, num_episodes, mqtt_client):
         """app/base.py:108-124: any Exception is logged and swallowed; the
         BaseException game errors propagate, as in the reference."""
@@ -173,6 +200,9 @@ class SimulatePuppet:
             self._is_simulating = True
             logging.info('Starting simulations')
             dataset = MQTTDataset(mqtt_client, self)
+            if self._rng_stream == 'global':
+                self._run_sequential(num_episodes, dataset)
+                return
             for payload in self.play_payloads(num_episodes):
                 dataset.push_payload(payload)
         except Exception as e:

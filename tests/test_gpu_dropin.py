@@ -173,3 +173,75 @@ def test_tree_set_spills_to_the_edge_pool():
     ta, tb = a.tree_arrays(0), b.tree_arrays(0)
     for key in ('pos', 'e0', 'k', 'term', 'tval', 'codes', 'P', 'Q', 'N'):
         assert np.array_equal(ta[key], tb[key]), key
+
+
+class _Client:
+    def __init__(self):
+        self.msgs = []
+
+    def publish(self, topic, payload, qos=0):
+        self.msgs.append((topic, json.loads(payload), qos))
+
+        class I:
+            mid = len(self.msgs)
+        return I()
+
+
+def test_puppet_global_stream_plays_the_reference_sequence():
+    """rng_stream='global' (VERDICT r3 #5): the episodes come out in the reference's order, every
+    draw from the one global np.random stream (app/base.py:113-120: episodes in sequence, the
+    referee's turn carried over).  Episode 1 after np.random.seed(s) is the game the batched engine
+    plays for seed s; episode 2 continues the stream (it is the drop-in stack's second episode, not
+    a reseeded game); the stream is left exactly where that run leaves it; the payloads carry the
+    reference's MQTT fields."""
+    import torch
+    from minitchess_alphazero_amd import erlyx_compat, puppet as pp
+    from minitchess_alphazero_amd.agent import RoundRobinReferee, SimpleAlphaZeroAgent
+    from minitchess_alphazero_amd.callbacks import InfoRecorder, MonteCarloInit
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import MinitChessEnvironment
+    from minitchess_alphazero_amd.network import Network
+    from minitchess_alphazero_amd.policy import SimpleAlphaZeroPolicy
+    pp.MINITCHESS_ALPHAZERO_VERSION = 'v-test'
+    sims, seed = 8, 11
+    torch.manual_seed(0)
+    net = Network()
+    p = pp.SimulatePuppet('u1', 'topic/eps', num_simulations=sims, rng_stream='global')
+    p.load_weights(net.state_dict(), 'w1')
+    p.remote_status = pp.MasterOfPuppetsStatus.SIMULATE
+    p.remote_version = 'v-test'
+    c = _Client()
+    np.random.seed(seed)
+    p.run_episodes(2, c)
+    st_puppet = np.random.get_state()
+    assert len(c.msgs) == 2 and not p.is_simulating()
+    assert all(m[1]['weights_version'] == 'w1' and m[1]['userid'] == 'u1' for m in c.msgs)
+    eps = [m[1]['episode'] for m in c.msgs]
+
+    eng = Engine(n_games=1, sims=sims, seed_base=seed)
+    eng.set_weights(net)
+    eng.play()
+    assert compare_records(eps[0], eng.episodes()[0])[2] is None
+
+    class DS:
+        def __init__(self):
+            self.episodes = []
+
+        def push(self, ep):
+            self.episodes.append(ep)
+
+    env = MinitChessEnvironment()
+    policy = SimpleAlphaZeroPolicy(network=net)
+    agents = [SimpleAlphaZeroAgent(env, policy, sims) for _ in range(2)]
+    ds = DS()
+    np.random.seed(seed)
+    erlyx_compat.run_episodes(env, RoundRobinReferee(agents), 2,
+                              callbacks=[InfoRecorder(ds), MonteCarloInit(agents[0]), MonteCarloInit(agents[1])])
+    st_direct = np.random.get_state()
+    assert compare_records(eps[1], ds.episodes[1])[2] is None
+    assert [r['reward'] for r in eps[1]] == [r['reward'] for r in ds.episodes[1]]
+    assert st_puppet[1].tobytes() == st_direct[1].tobytes() and st_puppet[2] == st_direct[2]
+    eng2 = Engine(n_games=1, sims=sims, seed_base=seed + 1)
+    eng2.set_weights(net)
+    eng2.play()
+    assert compare_records(eps[1], eng2.episodes()[0])[2] is not None    # not a reseeded game

@@ -177,3 +177,14 @@ def test_learn_puppet_weights_dict_is_reference_format():
     d = lp.get_weights_dict()
     assert set(d) == {'weights', 'version'} and isinstance(d['weights'], str)
     _same(wire.decode_weights(d['weights']), lp.weights)
+
+
+def test_puppet_rng_stream_modes():
+    """SimulatePuppet's rng_stream: 'batched' (default, parallel games, one seed draw per batch) or
+    'global' (the reference's sequential stream, app/base.py:113-120); anything else is refused
+    before any engine exists."""
+    from minitchess_alphazero_amd import puppet as pp
+    assert pp.SimulatePuppet('u', 't')._rng_stream == 'batched'
+    assert pp.SimulatePuppet('u', 't', rng_stream='global')._rng_stream == 'global'
+    with pytest.raises(ValueError):
+        pp.SimulatePuppet('u', 't', rng_stream='per-game')
