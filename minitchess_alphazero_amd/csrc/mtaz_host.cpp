@@ -1313,7 +1313,7 @@ extern "C" int mtaz_diag_select_stamps(unsigned long long* out8, int reset) {
 
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
-  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 2 || variant == 3;
+  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 2 || variant == 3 || variant == 5;
   if (h->precision == NET_F16F8)
     ok = ok || variant == 1 || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 ||
          variant == 33554432 || variant == 8388608 + 16777216 + 33554432;

@@ -179,7 +179,8 @@ __device__ __forceinline__ T sel4(int b, T x0, T x1, T x2, T x3) {
 }
 
 // VAR: 0 = product; 1 = class tiles without the tap skip (every MFMA runs: the bit-identity
-// reference of the skip, and its A/B)
+// reference of the skip, and its A/B); 2 = the tail instances as first built in round 4 (off-board
+// cells on the padding squares, weights one k-block ahead), for the A/B of the round-4b tails
 template <bool STAMP, int VAR, int NVB = XB>
 __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev& D, const NetWeights& W,
                                            const Pos* __restrict__ pos, const int32_t* __restrict__ count,
@@ -189,6 +190,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   using namespace ny;
   static_assert(NVB >= 1 && NVB <= XB, "boards per workgroup");
   constexpr bool SKIP = NVB == XB && (VAR & 1) == 0;
+  constexpr bool TAIL_R3 = (VAR & 2) != 0;   // tails with the first round-4 build's zero cells and weight ring
   int b0, nb;
   {   // tail-balanced board assignment (round 3): full rounds of 4 boards, then 1-3 per CU
     const int n = count ? *count : max_b;
@@ -361,6 +363,10 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
     *reinterpret_cast<uint4*>(smem + cell(bb, r) + 256 * q + part * PART_B) = make_uint4(0, 0, 0, 0);
   }
   for (int i = tid; i < 2 * XB * IROWS; i += NT) *reinterpret_cast<uint4*>(simg + i * 16) = make_uint4(0, 0, 0, 0);
+  if constexpr (NVB < XB) {   // board 3 (unused by the tail instances): half 0 zero, the off-board cells of every residue
+    for (int i = tid; i < 2 * 32 * 16; i += NT)
+      *reinterpret_cast<uint4*>(smem + 3 * BOARD_B + (i >> 9) * PART_B + 16 * (i & 511)) = make_uint4(0, 0, 0, 0);
+  }
   {   // the fragment offset table [tap 9][half 2][lane 64][tile i 4]: the byte offset of chunk g of
       // the source square's cell on the board, of a zero cell (zcell) off it and for the padding
       // squares
@@ -372,7 +378,11 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         const int v = tile_bp<NVB>(4 * h + i, ln & 15), b = v & 3, p = v >> 2, gg = ln >> 4;
         const int dh = tap / 3 - 1, dw = tap % 3 - 1, r = p / 5 + dh, c = p % 5 + dw, s = p + 5 * dh + dw;
         const bool valid = p < 30 && (unsigned)r < 6u && (unsigned)c < 5u;
-        ent = (valid ? cell(b, s) : zcell(s + 4 * b)) + 256 * gg;
+        // off the board: a zero cell on the bank group the source would have had -- for the tail
+        // instances any of board 3's (unused, zeroed) half 0, for 4 boards a padding square (bank
+        // groups 2, 3 mod 4 only: tools/net_tiles.py)
+        const int zc = (NVB < XB && !TAIL_R3) ? cell(3, (s + 4 * b + 4) & 15) : zcell(s + 4 * b);
+        ent = (valid ? cell(b, s) : zc) + 256 * gg;
       }
       tab[e] = ent;
     }
@@ -458,7 +468,13 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   // (half-0 tiles in the chunk's last half-step, half-1 tiles in the next chunk's first one).  The
   // row-gated tile (T in half 0, B in half 1) runs last, behind one uniform branch.
   const int tab_l = IMG_B + AUXB + 16 * lane;
-  f16x8 A[2][2 * CT], BH[2][8];
+  // the weight ring: RS slots, loads PD k-blocks ahead.  A 4-board k-block runs 60-96 MFMAs, which
+  // cover one k-block of load latency; a tail instance's runs 12 x NVB, so its loads go further
+  // ahead into the registers its fewer fragment tiles leave free (round 3's depths 5 / 3 / 2).
+  // RS divides the 24 k-blocks of a tap row, so a k-block's slot is the same in every row.
+  constexpr int PD = TAIL_R3 ? 1 : NVB == 1 ? 5 : NVB == 2 ? 3 : NVB == 3 ? 2 : 1, RS = PD + 1;
+  static_assert(24 % RS == 0, "weight ring");
+  f16x8 A[RS][2 * CT], BH[2][8];
   uint4 tpre;     // table entries of the half-step after next (read during the current one)
   int onx[4];     // table entries (fragment bases, k-block step aside) of the next half-step
   // weights k-block-major (NetWeights::convyk): the wave's fragment (channel tile ct, part) of
@@ -474,10 +490,12 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   for (int L = 0; L < CONV_LAYERS; ++L) {
     // layer prologue: k-block 0's weights, half-step (0, 0)'s fragments, the offsets of (0, 1)
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      wload(A[0][2 * c], 0, c, 0);
-      wload(A[0][2 * c + 1], 0, c, 1);
-    }
+    for (int kp = 0; kp < PD; ++kp)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        wload(A[kp][2 * c], kp, c, 0);
+        wload(A[kp][2 * c + 1], kp, c, 1);
+      }
     {
       const uint4 e0 = *reinterpret_cast<const uint4*>(smem + tab_l);
       const uint4 e1 = *reinterpret_cast<const uint4*>(smem + tab_l + 1024);
@@ -514,7 +532,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         constexpr bool need0 = act(NVB, SKIP, U1r, 4 * H1 + 0), need1 = act(NVB, SKIP, U1r, 4 * H1 + 1);
         constexpr bool need2 = act(NVB, SKIP, U1r, 4 * H1 + 2), need3 = act(NVB, SKIP, U1r, 4 * H1 + 3);
         constexpr int NFR = 2 * (need0 + need1 + need2 + need3);
-        // + the table read + (half 0) all 8 weight loads of k-block U + 1: a full k-block of MFMAs
+        // + the table read + (half 0) all 8 weight loads of k-block U + PD: a full k-block of MFMAs
         // then covers their latency (a k-block runs 60-96 MFMAs with the tap skip)
         constexpr int NW_ = H == 0 ? 2 * CT : 0;
         constexpr int NQ = NFR + 1 + NW_;
@@ -532,8 +550,8 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         int o[4] = {onx[0], onx[1], onx[2], onx[3]};
         f16x8 (&BC)[8] = BH[H];
         f16x8 (&BN)[8] = BH[H1];
-        f16x8 (&AC)[2 * CT] = A[U & 1];
-        f16x8 (&AN)[2 * CT] = A[(U + 1) & 1];
+        f16x8 (&AC)[2 * CT] = A[U % RS];
+        f16x8 (&AN)[2 * CT] = A[(U + PD) % RS];
         // group kq issues memory items [q0, q1) and adds [a0, a1)
         sfor<0, NG>([&](auto k_c) __attribute__((always_inline)) {
           constexpr int KQ = decltype(k_c)::value;
@@ -554,9 +572,9 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
             } else if constexpr (Q == NFR) {   // the table entries of (U2, H2)
               const int ta = U2 < 24 ? tab_j + (U2 / 8) * 2048 + H2 * 1024 : tab_n + ((U2 - 24) / 8) * 2048 + H2 * 1024;
               tpre = *reinterpret_cast<const uint4*>(smem + ta);
-            } else {                           // weight load: k-block U + 1, channel tile / part
+            } else {                           // weight load: k-block U + PD, channel tile / part
               constexpr int W_ = Q - NFR - 1, ct = W_ >> 1, part = W_ & 1;
-              const int kbn = U + 1 < 24 ? kb_j + U + 1 : (j < 2 ? kb_j + 24 : KBY - 1);
+              const int kbn = kb_j + U + PD < KBY ? kb_j + U + PD : KBY - 1;   // (clamped: the layer's last k-blocks)
               wload(AN[2 * ct + part], kbn, ct, part);
             }
           });
@@ -718,7 +736,9 @@ static int device_cus_y() {
 
 // variant 0: the product (full rounds of 4 boards, then the tail launch); 1: 4 boards per
 // workgroup throughout (no tail); 2: class tiles without the tap skip, 4 boards throughout;
-// 3: round 3's kernel (mtaz_net16_r3.hip, main + tail)
+// 3: round 3's kernel (mtaz_net16_r3.hip, main + tail); 5: the product with the first round-4
+// build's tail instances (VAR bit 2: off-board cells on the padding squares, 2-way bank conflicts;
+// weights one k-block ahead)
 void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
                       float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
                       int variant) {
@@ -734,6 +754,11 @@ void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const i
     hipLaunchKernelGGL((k_net_y<false, 0, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, ncu);
     hipLaunchKernelGGL((k_net_y_tail<0>), dim3(3 * ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, ncu);
+  } else if (variant == 5 && ncu > 0) {
+    hipLaunchKernelGGL((k_net_y<false, 0, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
+                       values_out, nullptr, ncu);
+    hipLaunchKernelGGL((k_net_y_tail<2>), dim3(3 * ncu), dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, ncu);
   } else if (variant == 2) {
     hipLaunchKernelGGL((k_net_y<false, 1, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,

@@ -107,7 +107,9 @@ class Engine:
         set_precision resets it).  f16x3 (k_net_y): 1 = 4 boards per workgroup in every round (no
         tail launch), 2 = the class tiles without the off-board tap skip, both bitwise equal to 0;
         3 = round 3's kernel (one stored-units exponent per workgroup; bitwise equal to 0 on nets
-        whose activations stay below 2^14).  f16f8 (k_net_z): 1 = 4 boards per workgroup in every
+        whose activations stay below 2^14), 5 = the product with the first round-4 tail instances
+        (off-board cells on the padding squares, 2-way LDS bank conflicts; weights one k-block
+        ahead; bitwise equal to 0).  f16f8 (k_net_z): 1 = 4 boards per workgroup in every
         round (no tail launches), 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross
         terms, 25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),
         33554432 = the round-2 epilogue (unscaled conversions), 58720256 = both (the round-2

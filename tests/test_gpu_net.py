@@ -122,7 +122,7 @@ def test_product_library_rejects_untested_variants():
     eng = Engine(n_games=4, sims=2)
     for prec, good, bad in (('f16f8', [0, 1, 8192, 2097152, 25165824, 33554432, 58720256],
                              [16384, 32768, 65536, 131072, 2048, 4194304, 8388608, 16777216]),
-                            ('f16x3', [0, 1, 2, 3],
+                            ('f16x3', [0, 1, 2, 3, 5],
                              [512, 4, 8, 1024, 114688, 16777216, 2048, 8192, 4096, 268435456, 16384, 32768])):
         eng.set_precision(prec)
         for v in good:
@@ -212,6 +212,10 @@ def test_tail_launches_bit_identical(net_kind, precision):
     """The tail-balanced board assignment (k_net_z, k_net_y: the boards beyond the full rounds of
     4 x CUs go to workgroups of 1, 2 or 3 boards) computes every board exactly as 4 boards per
     workgroup do (variant 1): batch sizes whose tails take each of the three tail builds and none.
+    k_net_y's tails read off-board sources from zeroed cells of the unused board 3 on the source's
+    own bank group and load weights 5 / 3 / 2 k-blocks ahead; variant 5 keeps the first round-4
+    tails (off-board cells on the padding squares, 2-way bank conflicts for half the tail's fragment
+    reads; weights one k-block ahead): bitwise the same.
     k_net_y keeps one stored-units exponent per board, so this holds for nets whose activations
     pass 2^14 too (wide, stress); k_net_z's is per workgroup (tested below 2^14 only)."""
     from minitchess_alphazero_amd.engine import Engine
@@ -230,10 +234,12 @@ def test_tail_launches_bit_identical(net_kind, precision):
         pos = np.stack([pos_from_fen(fens[i % len(fens)]) for i in range(n)])
         eng.set_net_variant(0)
         l0, v0 = eng.evaluate(pos)
-        eng.set_net_variant(1)
-        l1, v1 = eng.evaluate(pos)
-        assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), n
-        assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), n
+        # 1: no tail launch; 5 (k_net_y): the tails' off-board cells on the padding squares
+        for var in ((1, 5) if precision == 'f16x3' else (1,)):
+            eng.set_net_variant(var)
+            l1, v1 = eng.evaluate(pos)
+            assert np.array_equal(l0.view(np.uint32), l1.view(np.uint32)), (n, var)
+            assert np.array_equal(v0.view(np.uint32), v1.view(np.uint32)), (n, var)
 
 
 def _tiny_activation_net(scale=2.0 ** -20):
