@@ -1,4 +1,4 @@
-"""World-size-2 gloo test of the sharding contract, CPU only.
+"""World-size-2 and -8 gloo tests of the sharding contract, CPU only.
 
 Each rank plays its shard of seeded games (oracle, synthetic evaluator) and the
 gathered records must equal a single-process run of the same global game ids; the
@@ -38,10 +38,12 @@ def _worker(rank, world, port, games_per_rank, sims, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_sharding_matches_single_process():
+@pytest.mark.parametrize('world,gpr', [(2, 2), (8, 1)])
+def test_rank_sharding_matches_single_process(world, gpr):
+    """World 2, and world 8 (the node size of BASELINE configs 4 and 5, one game per rank)."""
     from oracle import selfplay
     from oracle.mcts import SyntheticEvaluator
-    world, gpr, sims = 2, 2, 4
+    sims = 4
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -56,7 +58,7 @@ def test_two_rank_sharding_matches_single_process():
     ev = SyntheticEvaluator(salt=1)
     single = [selfplay.play_games(ev, 1, sims, seed_base=g)[0] for g in range(world * gpr)]
     assert flat == single
-    assert secs == 2.0
+    assert secs == float(world)
     assert tot['games'] == world * gpr and tot['plies'] == sum(len(r) for r in single)
 
 
