@@ -496,6 +496,11 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
               if (q + (uint32_t)k <= T.pool_cap) {
                 ne0 = T.pool_base + q;
               } else {
+                // the pool is exhausted: the call fails (ERR_EDGES), but the node is already in the
+                // hash; until the move ends, later visits must find a valid header, not whatever
+                // the slot held (an earlier play's edge range, possibly beyond a smaller pool):
+                // a terminal of value 0 backs up harmlessly
+                T.node_hdr[nbase + nn] = NodeHdr{0u, 0u, HDR_TERM, 0.0f};
                 atomicOr(D.pr.err, ERR_EDGES);
                 nn = NONE;
               }
