@@ -22,7 +22,8 @@
 //     chosen from board b's own bound, so no runtime max crosses boards: a board's results do not
 //     depend on which boards share its workgroup, for every net (round 3: only below 2^14).
 //
-// Workgroup = 4 boards (NVB < 4: the tail instances, per-board tiles as in round 3), 256 threads.
+// Workgroup = 4 boards (NVB < 4: the tail instances; 1 and 2 boards on round 3's per-board tiles,
+// 3 boards on class tiles of their own, TMAP3), 256 threads.
 // Wave w owns output channels [64w, 64w + 64) as 4 channel tiles of 16, times 8 N tiles of 16
 // squares: 32 accumulator tiles (128 AGPRs) + 32 master sums.  A conv's K = 2304 runs as 72
 // k-blocks of 32 contiguous k = tap*256 + ci (tap = 3(dr + 1) + (dc + 1)), in 3 rows of taps
@@ -89,22 +90,45 @@ __constant__ uint8_t TMAP4[8][16] = {
     {19, 117, 121, 125, 16, 118, 122, 126, 17, 119, 123, 127, 18, 116, 120, 124},
     {113, 102, 106, 110, 114, 103, 107, 111, 115, 100, 104, 108, 112, 101, 105, 109}};
 
-// (board | square << 2) of lane n of tile t = 4 half + i; the tail instances (NVB < 4) keep
-// round 3's per-board tiles: tile (half h, i) = board i, squares 16 h + n
-template <int NVB>
+// The 3-board tail instance's class tiles (round 4b; tools/net_tiles.py build3, checked there):
+// t0, t1 interior squares; t2 = T + 4 X squares (skips the tap dr = -1, dc = +1: gated in tap row
+// 0); t4 = L + 4 interior; t5 = R + 4 X (no dc = +1 taps); t6 = B + 4 X (skips dr = +1, dc = +1:
+// gated in tap row 2).  49 of 54 tile-taps run.  Under the (square + 4 board) bank rotation t0, t1
+// and t5 keep 1, 2 and 3 duplicate bank groups (2-way conflicts on those reads).
+__constant__ uint8_t TMAP3[8][16] = {
+    {49, 53, 94, 46, 50, 69, 88, 28, 32, 85, 25, 29, 48, 52, 26, 45},
+    {34, 54, 72, 74, 65, 84, 73, 92, 66, 70, 89, 93, 33, 86, 90, 30},
+    {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 18, 116, 120, 124},
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {64, 68, 42, 61, 80, 20, 24, 62, 81, 21, 40, 44, 82, 22, 41, 60},
+    {98, 117, 57, 76, 16, 38, 58, 77, 96, 36, 121, 78, 97, 37, 56, 125},
+    {113, 102, 106, 110, 114, 118, 122, 126, 17, 100, 104, 108, 112, 101, 105, 109},
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
+
+// (board | square << 2) of lane n of tile t = 4 half + i; the 1- and 2-board tail instances (and
+// the 3-board one of variant 5) keep round 3's per-board tiles: tile (half h, i) = board i,
+// squares 16 h + n
+template <int NVB, bool CLS3>
 __device__ __forceinline__ int tile_bp(int t, int n) {
   if constexpr (NVB == XB) return TMAP4[t][n];
+  if constexpr (CLS3) return TMAP3[t][n];
   return (t & 3) | ((16 * (t >> 2) + n) << 2);
 }
 
-// Compile-time activity of tile t at k-block u (0..23) of a tap row (dc = u / 8 - 1).  T (3) and
-// B (7) depend on the row (dr) and are gated at run time.
+// Compile-time activity of tile t at k-block u (0..23) of a tap row (dc = u / 8 - 1).  4 boards:
+// T (3) and B (7) depend on the row (dr) and are gated at run time.  3 boards (class tiles): t5
+// runs no dc = +1 k-block; t2 and t6 skip theirs in tap row 0 and 2 (gated).
 constexpr bool act(int nvb, bool skip, int u, int t) {
-  if (nvb < XB) return (t & 3) < nvb;
+  if ((t & 3) >= nvb) return false;
   if (!skip) return true;
-  return t == 5 ? u >= 8 : (t == 2 || t == 6) ? u < 16 : true;
+  if (nvb == XB) return t == 5 ? u >= 8 : (t == 2 || t == 6) ? u < 16 : true;
+  return t == 5 ? u < 16 : true;
 }
-constexpr bool gated(int nvb, bool skip, int t) { return nvb == XB && skip && (t == 3 || t == 7); }
+constexpr bool gated(int nvb, bool skip, int u, int t) {
+  if (!skip) return false;
+  if (nvb == XB) return t == 3 || t == 7;
+  return (t == 2 || t == 6) && u >= 16;
+}
 // the first k-block of the 12-k-block chunk holding u at which tile t runs (its MFMA chain of the
 // chunk starts there from C = 0)
 constexpr int first_u(int nvb, bool skip, int u, int t) {
@@ -189,8 +213,9 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
                                            int ncu) {
   using namespace ny;
   static_assert(NVB >= 1 && NVB <= XB, "boards per workgroup");
-  constexpr bool SKIP = NVB == XB && (VAR & 1) == 0;
-  constexpr bool TAIL_R3 = (VAR & 2) != 0;   // tails with the first round-4 build's zero cells and weight ring
+  constexpr bool TAIL_R3 = (VAR & 2) != 0;   // tails as first built in round 4 (per-board tiles, zero cells, ring)
+  constexpr bool CLS3 = NVB == 3 && !TAIL_R3;  // the 3-board instance on class tiles (round 4b)
+  constexpr bool SKIP = (NVB == XB || CLS3) && (VAR & 1) == 0;
   int b0, nb;
   {   // tail-balanced board assignment (round 3): full rounds of 4 boards, then 1-3 per CU
     const int n = count ? *count : max_b;
@@ -226,7 +251,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   uint32_t bp_lo = 0, bp_hi = 0;
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const uint32_t v = (t & 3) < NVB ? (uint32_t)tile_bp<NVB>(t, n) : (31u << 2);
+    const uint32_t v = (t & 3) < NVB ? (uint32_t)tile_bp<NVB, CLS3>(t, n) : (31u << 2);
     if (t < 4) bp_lo |= v << (8 * t); else bp_hi |= v << (8 * (t - 4));
   }
   auto bp_of = [&](int t) -> int { return (int)(((t < 4 ? bp_lo : bp_hi) >> (8 * (t & 3))) & 0xffu); };
@@ -300,7 +325,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         y[3] = relu_bits(__builtin_fmaf(a[3], is, bu.w * sv));
         // the padding squares 30, 31 (tile X; the tail instances' half-1 tiles) store zeros: they
         // are the zero cells of the off-board taps (masked, no branch)
-        if (NVB == XB ? t == 6 : t >= 4) {
+        if (NVB == XB ? t == 6 : CLS3 ? true : t >= 4) {
           const int keep = -(int)(p < 30);
 #pragma unroll
           for (int j = 0; j < 4; ++j) y[j] = __int_as_float(__float_as_int(y[j]) & keep);
@@ -375,7 +400,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
       const int i = e & 3, ln = (e >> 2) & 63, h = (e >> 8) & 1, tap = e >> 9;
       int ent = 0;
       if (i < NVB) {
-        const int v = tile_bp<NVB>(4 * h + i, ln & 15), b = v & 3, p = v >> 2, gg = ln >> 4;
+        const int v = tile_bp<NVB, CLS3>(4 * h + i, ln & 15), b = v & 3, p = v >> 2, gg = ln >> 4;
         const int dh = tap / 3 - 1, dw = tap % 3 - 1, r = p / 5 + dh, c = p % 5 + dw, s = p + 5 * dh + dw;
         const bool valid = p < 30 && (unsigned)r < 6u && (unsigned)c < 5u;
         // off the board: a zero cell on the bank group the source would have had -- for the tail
@@ -512,7 +537,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
       const int tab_j = tab_l + 6144 * j;
       const int tab_n = j < 2 ? tab_j + 6144 : tab_j;   // the next row's table (clamped in-bounds)
       const int kb_j = 24 * j;
-      if constexpr (SKIP) {
+      if constexpr (SKIP && NVB == XB) {
         if (j == 0) {   // T runs no k-block of row 0: its (stale) chunk sums must add zeros
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) acc[ct * 8 + 3] = (f32x4v){0};
@@ -522,10 +547,10 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         constexpr int S = decltype(s_c)::value, U = S >> 1, H = S & 1;
         // the next half-step (U1, H1) and the one after (U2, H2), within the row or the next one
         constexpr int U1 = H ? U + 1 : U, H1 = H ^ 1, U2 = U + 1, H2 = H;
-        constexpr int ACTN = (act(NVB, SKIP, U, 4 * H + 0) && !gated(NVB, SKIP, 4 * H + 0)) +
-                             (act(NVB, SKIP, U, 4 * H + 1) && !gated(NVB, SKIP, 4 * H + 1)) +
-                             (act(NVB, SKIP, U, 4 * H + 2) && !gated(NVB, SKIP, 4 * H + 2)) +
-                             (act(NVB, SKIP, U, 4 * H + 3) && !gated(NVB, SKIP, 4 * H + 3));
+        constexpr int ACTN = (act(NVB, SKIP, U, 4 * H + 0) && !gated(NVB, SKIP, U, 4 * H + 0)) +
+                             (act(NVB, SKIP, U, 4 * H + 1) && !gated(NVB, SKIP, U, 4 * H + 1)) +
+                             (act(NVB, SKIP, U, 4 * H + 2) && !gated(NVB, SKIP, U, 4 * H + 2)) +
+                             (act(NVB, SKIP, U, 4 * H + 3) && !gated(NVB, SKIP, U, 4 * H + 3));
         constexpr int NG = 3 * ACTN;                       // groups of 4 MFMAs
         constexpr int U1r = U1 < 24 ? U1 : U1 - 24;        // the next half-step's k-block in its row
         // fragment reads of (U1, H1): tiles active there at compile time or gated
@@ -541,7 +566,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         constexpr bool ADD0 = H == 1 && (U == 11 || U == 23);   // half-0 tiles' chunk sums
         constexpr bool ADD1 = H == 0 && (U == 0 || U == 12);    // half-1 tiles' (previous chunk)
         constexpr int NADD = (ADD0 || ADD1) ? 16 : 0;
-        if constexpr (SKIP && S == 1) {   // B runs no k-block of row 2: zero it after its last add
+        if constexpr (SKIP && NVB == XB && S == 1) {   // B runs no k-block of row 2: zero it after its last add
           if (j == 2) {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) acc[ct * 8 + 7] = (f32x4v){0};
@@ -590,7 +615,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
             constexpr int i = [] {
               int c = 0;
               for (int k = 0; k < 4; ++k)
-                if (act(NVB, SKIP, U, 4 * H + k) && !gated(NVB, SKIP, 4 * H + k) && c++ == ii) return k;
+                if (act(NVB, SKIP, U, 4 * H + k) && !gated(NVB, SKIP, U, 4 * H + k) && c++ == ii) return k;
               return 0;
             }();
             constexpr int t = 4 * H + i;
@@ -600,9 +625,12 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
           });
         });
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (gated(NVB, SKIP, 4 * H + 3)) {
-          constexpr int i = 3, t = 4 * H + i;
-          constexpr bool fu = U == 0 || U == 12;
+        // the row-gated tile: 4 boards T / B (i = 3, whole rows: a chunk's chain may start here),
+        // 3 boards t2 / t6 (i = 2, the dc = +1 k-blocks 16-23: never a chunk's first)
+        constexpr int GI = NVB == XB ? 3 : 2;
+        if constexpr (gated(NVB, SKIP, U, 4 * H + GI)) {
+          constexpr int i = GI, t = 4 * H + i;
+          constexpr bool fu = NVB == XB && (U == 0 || U == 12);
           if (j != (H ? 2 : 0)) {
             sfor<0, 12>([&](auto m_c) __attribute__((always_inline)) {
               constexpr int M = decltype(m_c)::value, ps = M / 4, ct = M % 4;

@@ -10,9 +10,10 @@ off-board source.
 
   4 boards (class tiles, TMAP4): zero cells are the padding squares 30, 31 (bank groups 2, 3 mod
       4 only), chosen on the source's bank group when one exists, else that group ^ 2.
-  1-3 boards (tail instances, per-board tiles): round 4b reads zeroed cells of the unused board 3
-      on the source's own bank group (product); --old: the padding squares as for 4 boards
-      (the first round-4 build, variant 5).
+  1-3 boards (tail instances): round 4b reads zeroed cells of the unused board 3 on the source's
+      own bank group, and the 3-board instance runs class tiles (TMAP3, a few duplicate bank
+      groups); --old: per-board tiles with the padding squares as zero cells (the first round-4
+      build, variant 5).
 
 Prints LDS cycles per instance over a conv's fragment reads and the conflict share (extra /
 total), the quantity SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE measures for the reads alone.
@@ -28,6 +29,14 @@ TMAP4 = [[64, 68, 72, 46, 65, 84, 24, 28, 32, 85, 25, 44, 48, 52, 26, 45],
          [83, 23, 42, 61, 80, 20, 43, 62, 81, 21, 40, 63, 82, 22, 41, 60],
          [19, 117, 121, 125, 16, 118, 122, 126, 17, 119, 123, 127, 18, 116, 120, 124],
          [113, 102, 106, 110, 114, 103, 107, 111, 115, 100, 104, 108, 112, 101, 105, 109]]
+TMAP3 = [[49, 53, 94, 46, 50, 69, 88, 28, 32, 85, 25, 29, 48, 52, 26, 45],
+         [34, 54, 72, 74, 65, 84, 73, 92, 66, 70, 89, 93, 33, 86, 90, 30],
+         [0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 18, 116, 120, 124],
+         [0] * 16,
+         [64, 68, 42, 61, 80, 20, 24, 62, 81, 21, 40, 44, 82, 22, 41, 60],
+         [98, 117, 57, 76, 16, 38, 58, 77, 96, 36, 121, 78, 97, 37, 56, 125],
+         [113, 102, 106, 110, 114, 118, 122, 126, 17, 100, 104, 108, 112, 101, 105, 109],
+         [0] * 16]
 PART_B = 16896
 BOARD_B = 2 * PART_B
 G128 = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
@@ -47,7 +56,7 @@ def zcell(wb):
 
 def entry(nvb, t, ln, tap, old):
     n, gg = ln & 15, ln >> 4
-    v = TMAP4[t][n] if nvb == 4 else ((t & 3) | ((16 * (t >> 2) + n) << 2))
+    v = TMAP4[t][n] if nvb == 4 else TMAP3[t][n] if (nvb == 3 and not old) else ((t & 3) | ((16 * (t >> 2) + n) << 2))
     b, p = v & 3, v >> 2
     dh, dw = tap // 3 - 1, tap % 3 - 1
     r, c, s = p // 5 + dh, p % 5 + dw, p + 5 * dh + dw
@@ -68,8 +77,10 @@ def cycles(addrs):
     return tot
 
 
-def active(t, tap):   # the 4-board tap skip (act() / gated())
+def active(t, tap, nvb=4):   # the tap skip (act() / gated())
     dr, dc = tap // 3 - 1, tap % 3 - 1
+    if nvb == 3:
+        return {0: True, 1: True, 2: (dr, dc) != (-1, 1), 4: True, 5: dc != 1, 6: (dr, dc) != (1, 1)}.get(t, False)
     return {0: True, 1: True, 2: dc != 1, 3: dr != -1, 4: True, 5: dc != -1, 6: dc != 1, 7: dr != 1}[t]
 
 
@@ -79,7 +90,7 @@ def main():
         tot = ideal = 0
         for tap in range(9):
             for t in range(8):
-                if (nvb == 4 and not active(t, tap)) or (nvb < 4 and (t & 3) >= nvb):
+                if (t & 3) >= nvb or ((nvb == 4 or (nvb == 3 and not old)) and not active(t, tap, nvb)):
                     continue
                 for kb in range(8):
                     for part in range(2):
