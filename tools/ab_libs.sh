@@ -1,7 +1,7 @@
 #!/bin/bash
 # In-process A/B of network variants in several experimental libraries (run through gpurun):
 #   bash tools/ab_libs.sh OUT "VARIANTS" lib1 lib2 ...
-# each lib is minitchess_alphazero_amd/libmtaz_<name>.so (same sources, other -D flags on the
+# each lib is minitchess_alphazero_amd/libmtaz_<name>.so (tools/build_exp_libs.py: same sources, other -D flags on the
 # network translation unit); results in gpurun_out/OUT/ab_<name>.json.  Stops at the first abnormal
 # exit; never retries.
 cd "${GRAFT_REPO_ROOT:-.}"
