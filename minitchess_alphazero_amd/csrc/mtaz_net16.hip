@@ -42,6 +42,14 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 namespace ny {
 
+// weight prefetch depth of the 1- and 2-board tail instances (k-blocks ahead; PD + 1 must divide
+// 24); build-time knobs for tools/build_exp_libs.py A/Bs, the product uses the defaults
+#ifndef MTAZ_Y_PD1
+#define MTAZ_Y_PD1 5
+#endif
+#ifndef MTAZ_Y_PD2
+#define MTAZ_Y_PD2 3
+#endif
 constexpr int KBY = 72;                     // k-blocks of 32 per conv
 constexpr int CELLS_B = 16384;              // per board and part: 32 squares x 32 chunks x 16 B
 constexpr int PART_B = CELLS_B + 512;       // + 512 B unused (round 3's zero line; keeps the heads' offset)
@@ -497,7 +505,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   // cover one k-block of load latency; a tail instance's runs 12 x NVB, so its loads go further
   // ahead into the registers its fewer fragment tiles leave free (round 3's depths 5 / 3 / 2).
   // RS divides the 24 k-blocks of a tap row, so a k-block's slot is the same in every row.
-  constexpr int PD = TAIL_R3 ? 1 : NVB == 1 ? 5 : NVB == 2 ? 3 : NVB == 3 ? 2 : 1, RS = PD + 1;
+  constexpr int PD = TAIL_R3 ? 1 : NVB == 1 ? MTAZ_Y_PD1 : NVB == 2 ? MTAZ_Y_PD2 : NVB == 3 ? 2 : 1, RS = PD + 1;
   static_assert(24 % RS == 0, "weight ring");
   f16x8 A[RS][2 * CT], BH[2][8];
   uint4 tpre;     // table entries of the half-step after next (read during the current one)
