@@ -1,6 +1,6 @@
-"""GPU: the driver's form `python bench.py --gpus N` end to end, N = 2 on the one-GPU box.
+"""GPU: the driver's form `python bench.py --gpus N` end to end, N = 2 and 8 on the one-GPU box.
 
-bench.py starts its own two ranks (minitchess_alphazero_amd.launch), both placed on cuda:0 with
+bench.py starts its own ranks (minitchess_alphazero_amd.launch), both placed on cuda:0 with
 --device 0 and gloo for the final reduction (RCCL needs one GPU per rank).  The JSON line must
 report n_gpus 2, both ranks' games in the whole-job value, and the usual roofline fields."""
 import json
@@ -15,9 +15,12 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-def test_bench_gpus_2_launches_its_ranks():
+@pytest.mark.parametrize('n', [2, 8])
+def test_bench_gpus_n_launches_its_ranks(n):
+    """N = 8 is BASELINE config 4's rank count (32,768 games on 8 GPUs) in miniature: eight ranks of
+    32 games on the one GPU, each pinned to its share of the box's cores."""
     env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
-    r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', '2', '--device', '0',
+    r = subprocess.run([sys.executable, os.path.join(REPO, 'bench.py'), '--gpus', str(n), '--device', '0',
                         '--dist-backend', 'gloo', '--games', '32', '--sims', '8', '--steps', '1', '--warmup', '0',
                         '--no-cpu-baseline', '--no-secondary'], env=env, capture_output=True, text=True,
                        timeout=240)
@@ -25,8 +28,8 @@ def test_bench_gpus_2_launches_its_ranks():
     lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d['n_gpus'] == 2 and d['scaling'] == 'weak'
+    assert d['n_gpus'] == n and d['scaling'] == 'weak'
     assert d['config']['games_per_gpu'] == 32
-    # whole-job value: both ranks' games over the max of the ranks' times
-    assert abs(d['value'] - 64 / (d['ms_per_step'] / 1e3)) <= 1e-6 * d['value']
+    # whole-job value: every rank's games over the max of the ranks' times
+    assert abs(d['value'] - 32 * n / (d['ms_per_step'] / 1e3)) <= 1e-6 * d['value']
     assert d['roofline']['avg_launch_ms'] > 0 and d['roofline_tree']['avg_launch_ms'] > 0
