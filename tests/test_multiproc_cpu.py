@@ -102,8 +102,10 @@ def _loop_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_loop_exchange_two_ranks():
-    world = 2
+@pytest.mark.parametrize('world', [2, 8])
+def test_loop_exchange_ranks(world):
+    """The C5 exchange at world 2 and 8 (config 5's rank count): records gathered to rank 0 in rank
+    order, rank 0's update broadcast to every rank."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
@@ -118,7 +120,7 @@ def test_loop_exchange_two_ranks():
         p.join(timeout=60)
         assert p.exitcode == 0
     parts = res[0][1]
-    assert [p[0] for p in parts] == [res[0][2], res[1][2]]          # rank order, intact
-    assert [p[1] for p in parts] == [res[0][3], res[1][3]]
-    assert res[1][1] is None
-    assert res[0][4] == res[1][4] and res[0][5] == res[1][5]           # identical weights after broadcast
+    assert [p[0] for p in parts] == [res[r][2] for r in range(world)]     # rank order, intact
+    assert [p[1] for p in parts] == [res[r][3] for r in range(world)]
+    assert all(res[r][1] is None for r in range(1, world))
+    assert all(res[0][4] == res[r][4] and res[0][5] == res[r][5] for r in range(world))   # identical weights
