@@ -1,4 +1,4 @@
-"""GPU: BASELINE config 5 (self-play -> learner -> weights) across ranks, world size 2.
+"""GPU: BASELINE config 5 (self-play -> learner -> weights) across ranks, world sizes 2 and 8.
 
 Two ranks started as bench.py --gpus N starts them (minitchess_alphazero_amd.launch), both on cuda:0
 of the one-GPU box, gloo for the exchange (records gathered to rank 0, one flat weight broadcast).
@@ -16,14 +16,16 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-def test_loop_two_ranks_equal_one_process(tmp_path):
+@pytest.mark.parametrize('world', [2, 8])
+def test_loop_ranks_equal_one_process(tmp_path, world):
+    """World 2, and world 8 (config 5's rank count in miniature, eight ranks on the one GPU)."""
     import torch
     from minitchess_alphazero_amd.launch import spawn_ranks
     from minitchess_alphazero_amd.loop import flat_weights, run_loop
     G, sims, iters = 8, 8, 2
     out = str(tmp_path / 'loop.json')
     env = dict(os.environ, MASTER_ADDR='127.0.0.1')
-    rc = spawn_ranks(2, [sys.executable, os.path.join(REPO, 'tests', 'rank_worker_loop.py'), out, str(G), str(sims),
+    rc = spawn_ranks(world, [sys.executable, os.path.join(REPO, 'tests', 'rank_worker_loop.py'), out, str(G), str(sims),
                          str(iters)], env=env)
     assert rc == 0
     res = json.load(open(out))
@@ -32,14 +34,14 @@ def test_loop_two_ranks_equal_one_process(tmp_path):
     torch.use_deterministic_algorithms(True)
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
     try:
-        hist, net = run_loop(iters, 2 * G, sims, batch_size=16, dist=None, device=0, seed=0, log=lambda s: None)
+        hist, net = run_loop(iters, world * G, sims, batch_size=16, dist=None, device=0, seed=0, log=lambda s: None)
     finally:
         torch.use_deterministic_algorithms(prev[0])
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev[1], prev[2]
     flat, _ = flat_weights(net, 'cpu')
     assert len(res['history']) == iters
     for a, b in zip(res['history'], hist):
-        assert a['games'] == b['games'] == 2 * G
+        assert a['games'] == b['games'] == world * G
         assert a['rows'] == b['rows']          # (weights_version is a timestamp, app/base.py)
         assert a['loss'] == b['loss'], (a['loss'], b['loss'])
     assert res['head'] == flat[:2000].tolist() and res['tail'] == flat[-2000:].tolist()
