@@ -52,7 +52,9 @@ def log(msg):
 def _cpu_game(job):
     """One seeded game of the oracle's restatement of the app/puppet CPU path (batch-1 torch-CPU
     fp32 per leaf, FEN-keyed dict tables, Python rules) on `threads` torch threads."""
-    sims, seed, threads = job
+    sims, seed, threads = job[:3]
+    if len(job) > 3 and job[3] is not None:
+        os.sched_setaffinity(0, {job[3]})   # one core of its own (the 1-thread legs)
     import torch
     torch.set_num_threads(threads)
     from oracle.mcts import TorchNetEvaluator
@@ -86,7 +88,32 @@ def host_cores():
             'usable': usable}
 
 
-def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budget=None):
+def one_thread_jobs(gpu_sims, extra_sims=()):
+    """The 1-thread legs of the full plan: every (sims, seed) game, one single-threaded process each."""
+    seeds = [0, 1, 2]
+    sims_list = sorted({32, gpu_sims, *extra_sims})
+    return [(sm, sd, 1) for sm in sims_list for sd in seeds], sims_list, seeds
+
+
+def start_one_thread_legs(gpu_sims, extra_sims=(), reserve=2):
+    """Start the 1-thread legs asynchronously, BEFORE this process touches the GPU, so
+    that they run during engine setup and the untimed warm-up steps and are collected before the
+    timed region starts.  Each game runs in its own spawned process (never exec'ed over this one),
+    pinned to its own core of this process's affinity mask, skipping the first `reserve` cores (the
+    GPU rank's main thread and host threads).  Returns (pool, async result, meta)."""
+    import multiprocessing as mp
+    jobs, sims_list, seeds = one_thread_jobs(gpu_sims, extra_sims)
+    cores = sorted(os.sched_getaffinity(0))
+    free = cores[reserve:] if len(cores) > reserve + len(jobs) else cores
+    jobs = [j + (free[i % len(free)] if len(free) >= len(jobs) else None,) for i, j in enumerate(jobs)]
+    pool = mp.get_context('spawn').Pool(len(jobs))
+    res = pool.map_async(_cpu_game, jobs, chunksize=1)
+    meta = {'sims_list': sims_list, 'seeds': seeds, 'cores': [j[3] for j in jobs], 't_start': elapsed()}
+    log(f'cpu baseline 1-thread legs started: {len(jobs)} games on cores {meta["cores"]}')
+    return pool, res, meta
+
+
+def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budget=None, one_thread=None):
     """seeded games (np.random.seed(g), random-init weights) at C1's 32 sims,
     the repo's default 36 (app/base.py:25) and the GPU's sims per move, each on all cores (games one
     after another, torch.set_num_threads = all_threads) and on 1 thread (all single-thread games at
@@ -135,7 +162,11 @@ def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budg
     for sims in others:
         if fits(f'{sims} sims all cores', len(seeds) * per_sim * sims * 1.25 + 5):
             all_cores(sims)
-    if plan == 'full':
+    if plan == 'full' and one_thread is not None:
+        # measured during the warm-up steps (start_one_thread_legs)
+        for sm in one_thread['sims_list']:
+            record(sm, '1thread', 1, one_thread['games'][sm])
+    elif plan == 'full':
         # 1 thread: every (sims, seed) game at once, one single-threaded process each (each game alone
         # on its core; measured at ~2.4x the all-core seconds per game)
         if fits('1-thread legs', per_sim * max(sims_list) * 2.6 * 1.2 + 8):
@@ -145,11 +176,17 @@ def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budg
             for i, sm in enumerate(sims_list):
                 record(sm, '1thread', 1, out[i * len(seeds):(i + 1) * len(seeds)])
     head = runs[f'{gpu_sims}sims/all']
+    sample = (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
+              f'{gpu_sims} sims/move on {all_threads} threads: the oracle restatement of app/puppet '
+              f'(batch-1 torch CPU fp32, dict tables, Python rules); value = games / total seconds')
+    if one_thread is not None:
+        sample += (f'.  The 1-thread runs ({", ".join(map(str, one_thread["sims_list"]))} sims x seeds '
+                   f'{one_thread["seeds"]}, one process per game pinned to cores {one_thread["cores"]}) ran '
+                   f'during the untimed engine setup and warm-up steps ({one_thread["overlap"]}), concurrently '
+                   f'with each other and with the GPU rank (whose host threads were limited to '
+                   f'{one_thread["gpu_host_threads"]} meanwhile), never during the timed region')
     return {'value': head['games_per_s'], 'unit': 'games/s', 'cores': all_threads, 'kind': 'port',
-            'sample': (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
-                       f'{gpu_sims} sims/move on {all_threads} threads: the oracle restatement of app/puppet '
-                       f'(batch-1 torch CPU fp32, dict tables, Python rules); value = games / total seconds'),
-            'sims_per_s': head['sims_per_s'], 'runs': runs}
+            'sample': sample, 'sims_per_s': head['sims_per_s'], 'runs': runs}
 
 
 def kernel_roofline(tot, prec):
@@ -186,7 +223,10 @@ def kernel_roofline(tot, prec):
             # the MFMA work the split actually issues, in dense-f16 equivalents (an e4m3 MFMA of the
             # block-scaled form runs at twice the f16 rate: 3 passes for f16x3, 1 + 2/2 for
             # f16+e4m3), over the same dense f16 peak: the MFMA pipes' utilisation
-            'issued_achieved': achieved * passes_eq, 'issued_frac': achieved * passes_eq / peak}
+            'issued_achieved': achieved * passes_eq, 'issued_frac': achieved * passes_eq / peak,
+            'issued_note': ('pass factor of the main launch (f16x3: 3 x 57/72 tile-taps) applied to every board: '
+                            'the 1- and 2-board tail instances run all 72 tile-taps and the 3-board one 49 of 54, '
+                            'so issued_* slightly understate the issued MFMA work (ADVICE r4)') if prec == 1 else None}
 
 
 def main():
@@ -231,6 +271,18 @@ def main():
                     help='N>1 end-of-run reductions: nccl (RCCL, one GPU per rank) or gloo (host; with '
                          '--device, a rehearsal of the N-rank path on one GPU)')
     ap.add_argument('--device', type=int, default=None, help='GPU of this rank (default LOCAL_RANK)')
+    ap.add_argument('--rank-share', type=int, default=0,
+                    help='run this one process at the host share one of N ranks on the node gets '
+                         '(launch.rank_host_share: usable CPUs / N): before anything touches the GPU, pin '
+                         'to that many cores of the affinity mask and use that many host threads '
+                         '(VERDICT r4 #2: the 8-rank host share measured on a 1-GPU box)')
+    ap.add_argument('--sync-mode', type=int, default=0, choices=[0, 1],
+                    help='how the engine waits for its stream: 0 = hipStreamSynchronize, 1 = blocking-sync '
+                         'event (Engine.set_sync_mode)')
+    ap.add_argument('--one-thread-during-warmup', type=int, default=1, choices=[0, 1],
+                    help='1 (default): run the CPU baseline 1-thread legs during engine setup and the '
+                         'untimed warm-up steps (collected before the timed region); 0: after the timed '
+                         'steps, budget permitting')
     args = ap.parse_args()
 
     # N ranks: under torch.distributed.run WORLD_SIZE must equal --gpus; without a launcher this
@@ -241,13 +293,31 @@ def main():
         build(verbose=False)                  # once for all ranks (hipcc only, no GPU call)
     world = main_or_spawn(args.gpus, __file__)
 
-    import numpy as np
-    import torch
     rank = int(os.environ.get('RANK', 0))
     local = int(os.environ.get('LOCAL_RANK', 0))
     # this rank's disjoint slice of the host cores and its host-thread budget (launch.rank_host_share)
-    from minitchess_alphazero_amd.launch import pin_rank
-    host_threads = pin_rank(local, int(os.environ.get('LOCAL_WORLD_SIZE', world)))
+    from minitchess_alphazero_amd.launch import pin_rank, rank_host_share
+    rank_share = None
+    if args.rank_share > 1:
+        # one rank's share of an N-rank node, emulated in this single process before any thread or GPU
+        # context exists: `threads` CPUs (usable // N) as the affinity mask and the thread budget
+        cores_all = sorted(os.sched_getaffinity(0))
+        _, thr = rank_host_share(0, args.rank_share)
+        os.sched_setaffinity(0, cores_all[:thr])
+        host_threads = thr
+        rank_share = {'ranks': args.rank_share, 'cores': cores_all[:thr], 'threads': thr}
+        log(f'rank share of {args.rank_share}: affinity {cores_all[:thr]}, {thr} host threads')
+    else:
+        host_threads = pin_rank(local, int(os.environ.get('LOCAL_WORLD_SIZE', world)))
+    # the CPU baseline's 1-thread legs run during setup and warm-up (rank 0 of a 1-GPU run), started
+    # before this process touches the GPU
+    legs = None
+    if (world == 1 and not args.no_cpu_baseline and args.cpu_plan == 'full' and args.one_thread_during_warmup
+            and rank_share is None):
+        extra = (args.default_sims,) if args.default_sims and args.default_sims != args.sims else ()
+        legs = start_one_thread_legs(args.sims, extra)
+    import numpy as np
+    import torch
     torch.set_num_threads(host_threads)
     dist = None
     device = local if args.device is None else args.device
@@ -300,7 +370,11 @@ def main():
     eng.set_net_variant(args.net_variant)
     eng.set_timing(True)
     eng.set_pipeline(args.groups)
+    eng.set_sync_mode(args.sync_mode)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
+    LEG_HOST_THREADS = 2
+    if legs is not None:
+        eng.set_host_threads(min(eng_threads, LEG_HOST_THREADS))   # leave the cores to the 1-thread legs
 
     def agree_max(x):
         """The max of x over ranks (budget decisions must be the same on every rank)."""
@@ -317,6 +391,22 @@ def main():
         warm_s.append(time.perf_counter() - t0)
         log(f'warmup {i + 1}/{args.warmup}: {warm_s[-1]:.2f} s')
     budget = {'limit_s': args.time_budget, 'skipped': []}
+    one_thread = None
+    if legs is not None:
+        pool, res, meta = legs
+        t_wait = elapsed()
+        out = res.get()
+        pool.close()
+        pool.join()
+        eng.set_host_threads(eng_threads)
+        waited = elapsed() - t_wait
+        per = len(meta['seeds'])
+        one_thread = {**meta, 'games': {sm: out[i * per:(i + 1) * per] for i, sm in enumerate(meta['sims_list'])},
+                      'gpu_host_threads': LEG_HOST_THREADS,
+                      'overlap': (f'{args.warmup} warm-up step(s); started at {meta["t_start"]:.1f} s, the timed '
+                                  f'region waited {waited:.1f} s more for them')}
+        budget['one_thread_legs_wait_s'] = round(waited, 1)
+        log(f'cpu baseline 1-thread legs done (waited {waited:.1f} s after the warm-up)')
     if warm_s:
         # the timed steps are the contract: if they cannot fit the budget, say so and stop before
         # timing rather than being killed without a line
@@ -338,11 +428,19 @@ def main():
     KEYS = ('sims', 'nn_evals', 'memo_hits', 'memo_batch_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
             'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms', 'choice_ms', 'gap_ms')
 
+    import resource
+
+    def cpu_s():
+        r = resource.getrusage(resource.RUSAGE_SELF)
+        return r.ru_utime + r.ru_stime
+
     def timed(engine, steps, label):
         """`steps` full self-play batches between barrier + synchronize; max wall over ranks and
-        summed counters (sharding.reduce_run)."""
+        summed counters (sharding.reduce_run).  tot['host_cpu_ms']: this process's CPU time (every
+        thread, user + system) over the region, summed over ranks."""
         tot = {k: 0.0 for k in KEYS}
         sync()
+        c0 = cpu_s()
         t0 = time.perf_counter()
         for i in range(steps):
             st = engine.play()
@@ -352,6 +450,7 @@ def main():
                 log(f'{label} step {i + 1}/{steps}: {st["wall_ms"] / 1e3:.2f} s')
         sync()
         dt = time.perf_counter() - t0
+        tot['host_cpu_ms'] = (cpu_s() - c0) * 1e3
         dt, tot = reduce_run(dt, tot, dist, red_device)
         return dt, tot, int(st.get('net_precision', 0))
 
@@ -418,15 +517,31 @@ def main():
         return
 
     roof = kernel_roofline(tot, prec)
-    traffic = None
+    # traffic: HBM/fabric bytes per launch from the PMC passes (tools/gpu.sh pmc -> tools/pmc_summary.py
+    # -> profiles/conv_traffic.json), attached only when those passes ran THIS library (the file's
+    # mtaz_src_sha256 stamp equals the loaded library's source hash) on this workload; else null, with
+    # the reason in traffic_source (a kernel change without a new PMC pass must not
+    # carry a stale figure)
+    from minitchess_alphazero_amd import _lib
+    lib_hash = _lib.lib().mtaz_version().decode().rsplit('mtaz-src-sha256=', 1)[-1]
+    traffic, why = None, f'no {os.path.relpath(args.traffic_json, HERE)}'
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get('games') == args.games and tj.get('sims') == args.sims and roof['kernel'].startswith(tj.get('kernel', '?')):
+            if tj.get('mtaz_src_sha256') != lib_hash:
+                why = (f'stale: PMC passes of library {str(tj.get("mtaz_src_sha256"))[:16]}, running '
+                       f'{lib_hash[:16]}')
+            elif not (tj.get('games') == args.games and tj.get('sims') == args.sims
+                      and roof['kernel'].startswith(tj.get('kernel', '?'))):
+                why = f'PMC passes of another workload ({tj.get("games")} games, {tj.get("sims")} sims, {tj.get("kernel")})'
+            else:
                 traffic = tj.get('hbm_bytes_per_launch')
-        except Exception:
-            traffic = None
+                why = (f'{os.path.relpath(args.traffic_json, HERE)}: PMC passes of this library '
+                       f'({lib_hash[:16]}) on this workload')
+        except Exception as e:
+            why = f'unreadable: {e}'
     roof['traffic'] = traffic
+    roof['traffic_source'] = why
     line = {
         'metric': METRIC,
         'value': games / dt,
@@ -469,7 +584,15 @@ def main():
         # (host_choice_s), apply, game states, move start, the first Dirichlet draws
         'host_gap_s': tot['gap_ms'] / 1e3,
         'host_choice_s': tot['choice_ms'] / 1e3,
+        # CPU time of this rank's process over the timed region (all threads): host_cpus_busy = the
+        # CPUs it keeps busy on average, against its share of the node (launch.rank_host_share)
+        'host_cpu_s': tot['host_cpu_ms'] / 1e3 / world,
+        'host_cpus_busy': tot['host_cpu_ms'] / 1e3 / world / dt,
+        'sync_mode': args.sync_mode,
+        'mtaz_src_sha256': lib_hash,
     }
+    if rank_share is not None:
+        line['rank_share'] = rank_share
     if secondary is not None:
         line['secondary'] = secondary
     if at_default is not None:
@@ -478,7 +601,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or line['host_cores']['usable']
         extra = (args.default_sims,) if args.default_sims and args.default_sims != sims else ()
-        cb = cpu_baseline(args.cpu_plan, threads, sims, extra, deadline=args.time_budget, budget=budget)
+        cb = cpu_baseline(args.cpu_plan, threads, sims, extra, deadline=args.time_budget, budget=budget,
+                          one_thread=one_thread)
         if cb is not None:
             line['cpu_baseline'] = cb
             line['vs_cpu_baseline'] = line['value'] / cb['value']

@@ -133,14 +133,20 @@ int mtaz_stats(mtaz_engine* h, double* out, int n);
  * network kernel for fp16x3) */
 int mtaz_set_timing(mtaz_engine* h, int on);
 /* network arithmetic: 1 = k_net_y (default), fp16x3 split MFMA, within 1e-5 of the reference on
- * every tested net; 2 = k_net_z, f16 Wh*Xh + e4m3 cross terms (within 1e-5 on the seed-0 and C3
- * nets only); 0 = fp32 MFMA */
+ * every tested net; 2 = k_net_z, f16 Wh*Xh + e4m3 cross terms: its scope is nets whose layer
+ * bounds stay below 2^14 (within 1e-5 on the seed-0 and C3 nets; past 2^14 its results depend on
+ * the batch and it refuses the leaf memo, mtaz_set_memo); 0 = fp32 MFMA */
 int mtaz_set_precision(mtaz_engine* h, int precision);
 /* game slot g of the next mtaz_play is seeded np.random.seed(seed_base + g) */
 int mtaz_set_seed_base(mtaz_engine* h, uint64_t seed_base);
 /* host threads of the per-move work (Dirichlet draws, action choice; 0 = the CPUs of the process's
  * affinity mask, at most 16).  Pipeline groups split them. */
 int mtaz_set_host_threads(mtaz_engine* h, int n);
+/* how the host thread waits for the engine's stream at its sync points (root states, visit counts,
+ * error flags): 0 = hipStreamSynchronize (default), 1 = an event created with hipEventBlockingSync,
+ * so the waiting thread sleeps instead of holding a CPU (8 ranks share one node's host cores:
+ * bench.py --sync-mode, --rank-share).  Results are identical in both modes. */
+int mtaz_set_sync_mode(mtaz_engine* h, int mode);
 /* network-only timing harness: avg ms over `iters` launches on n device positions; with
  * stamped != 0 also per-workgroup [nwg][stem, conv K loops, epilogues, heads cycles, total
  * cycles, total 100 MHz ticks] from a separate diagnostic build (tools/bench_net.py) */
@@ -168,7 +174,12 @@ int mtaz_set_pipeline(mtaz_engine* h, int groups);
  * every table, visit count and move is unchanged, the network runs on fewer leaves.  Mode 2 also
  * keeps every evaluated position of the play (all games, until the next mtaz_play, mtaz_clear_trees
  * of all tables or mtaz_set_weights) in an HBM table that later simulations of any game read.  Off
- * automatically when the agents use different weight slots (mtaz_set_agent_slots). */
+ * automatically when the agents use different weight slots (mtaz_set_agent_slots).
+ * A memo hit hands on a result computed in another network launch, which is exact for precisions 0
+ * and 1 (every board computed independently of its batch).  Precision 2 (k_net_z) keeps one
+ * dynamic-range exponent per workgroup: once a layer's bound passes 2^14 its results depend on the
+ * other boards of the workgroup, so a play with memo >= 1 that reaches that range fails
+ * (MTAZ_E_CAPACITY, "f16f8-range-with-memo"); with memo 0 it plays, outside the sharding identity. */
 int mtaz_set_memo(mtaz_engine* h, int mode);
 /* Edge storage of the MCTS tables (exp/agent.py:29-36 keeps a list of Q/N/P per node; here a
  * node's children are a contiguous edge range).  Each of the 2 * n_games tables owns a region of
@@ -219,7 +230,10 @@ int mtaz_tree_get(mtaz_engine* h, int tree, uint32_t* pos, uint32_t* e0, uint16_
                   uint16_t* codes, float* P, double* Q, uint32_t* N);
 /* load a table from the mtaz_tree_get layout (n nodes; the hash index and visit sums are rebuilt):
  * moves a MonteCarloTreeSearch into a larger engine when a later simulate() asks for more
- * simulations than its first (exp/agent.py:41-45 has no such limit) */
+ * simulations than its first (exp/agent.py:41-45 has no such limit).  Edges that do not fit the
+ * table's own region take a fresh block of the shared pool; pool edges the replaced table held are
+ * NOT returned (as for a partial mtaz_clear_trees): load into a cleared table, and reclaim the pool
+ * with a clear of all tables (mtaz_clear_trees(h, NULL, 0); mtaz_play does one) */
 int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* pos, const uint32_t* e0, const uint16_t* k,
                   const uint8_t* term, const double* tval, const uint16_t* codes, const float* P, const double* Q,
                   const uint32_t* N);

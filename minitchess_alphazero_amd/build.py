@@ -5,7 +5,8 @@ csrc/mtaz_net8.hip (network kernels k_net_y, k_net_z), csrc/mtaz_host.cpp (C ABI
 RNG compiled with -ffp-contract=off, engine driver) and csrc/mtaz_wire.cpp (episode wire
 format).  The shared object lands next to this file so it travels to the GPU box with the repo
 snapshot.  build(diag=True) makes libmtaz_diag.so with -DMTAZ_NET_DIAG: the network kernels'
-A/B and timing-only variants (tools/bench_net.py --diag), never loaded by the product path.
+A/B and timing-only variants and round 3's k_net_y (csrc/mtaz_net16_r3.hip, variant 3; the
+round-3 comparison tests load it in a child process), never loaded by the product path.
 
 Build fingerprint: source_hash() is the sha256 of every file under csrc/, include/mtaz.h and the
 compile commands below.  It is compiled into the library (mtaz_version() ends in "src=<hash>"),
@@ -32,7 +33,9 @@ SOURCES = [
     # (16K) the tail instantiations (fewer boards) were left rolled, and their accumulator arrays
     # went to scratch (round 3: k_net_y<., ., 3> 14x slower)
     ('mtaz_net16.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
-    ('mtaz_net16_r3.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
+    # round 3's k_net_y (f16x3 variant 3): a bit-identity and batch-dependence reference only, so it
+    # is compiled into the diagnostic library alone
+    ('mtaz_net16_r3.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000', 'DIAG_ONLY']),
     ('mtaz_net8.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
     ('mtaz_wire.cpp', ['-O2']),
@@ -87,6 +90,10 @@ def build(force=False, verbose=True, diag=False):
     objs = []
     procs = []
     for src, flags in SOURCES:
+        if 'DIAG_ONLY' in flags:
+            if not diag:
+                continue
+            flags = [f for f in flags if f != 'DIAG_ONLY']
         obj = os.path.join(bdir, src + '.o')
         cmd = [hipcc, '-x', 'hip', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-c',
                os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function',

@@ -212,6 +212,10 @@ enum NetPrecision { NET_FP32 = 0, NET_F16X3 = 1, NET_F16F8 = 2 };
 constexpr size_t CONV8_U4_PER_LAYER = (size_t)16 * 9 * 2 * 2 * 2 * 64;   // 73,728 x 16 B = 1.18 MB
 constexpr size_t CONV6_U4_PER_LAYER = (size_t)16 * 36 * 112;   // 64,512 x 16 B = 1.03 MB
 constexpr int ERR_F16 = 512;   // activation exceeded the f16 range in the fp16x3 trunk
+// k_net_z's one stored-units exponent per WORKGROUP left 0 (a bound passed 2^14): its results then
+// depend on the boards sharing the workgroup.  An error only where a leaf memo would hand such a
+// result to another batch (check_err(h, true) with memo >= 1); evaluate paths clear it.
+constexpr int ERR_ZRANGE = 1024;
 
 struct NetBuffers {
   float* x0;              // [B][256][32]

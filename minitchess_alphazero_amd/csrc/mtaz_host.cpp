@@ -660,9 +660,15 @@ struct mtaz_engine {
   int agent_slot[2] = {0, 0};
   int memo = 1;                         // leaf memo mode (mtaz_set_memo; Params::memo)
   int host_threads = default_host_threads();   // per-move host work (mtaz_set_host_threads)
+  // how the host thread waits for its stream (mtaz_set_sync_mode): 0 = hipStreamSynchronize (HIP's
+  // default wait), 1 = an event created with hipEventBlockingSync (the thread sleeps until the GPU
+  // signals, leaving its CPU to the other ranks' host work)
+  int sync_mode = 0;
+  hipEvent_t sync_ev = nullptr;
 
   ~mtaz_engine() {
     group_pool.reset();
+    if (sync_ev) (void)hipEventDestroy(sync_ev);
     for (mtaz_engine* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     if (noise_host) (void)hipHostFree(noise_host);
@@ -866,12 +872,27 @@ extern "C" mtaz_engine* mtaz_create(int device, int n_games, int sims, double cp
 
 extern "C" void mtaz_destroy(mtaz_engine* h) { delete h; }
 
-static int check_err(mtaz_engine* h) {
+// Wait for the engine's stream (every host sync point of the engine goes through here).
+static hipError_t stream_wait(mtaz_engine* h) {
+  if (h->sync_mode == 0) return hipStreamSynchronize(h->stream);
+  if (!h->sync_ev) {
+    const hipError_t e = hipEventCreateWithFlags(&h->sync_ev, hipEventBlockingSync | hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  const hipError_t e = hipEventRecord(h->sync_ev, h->stream);
+  return e != hipSuccess ? e : hipEventSynchronize(h->sync_ev);
+}
+
+// memo_path: the call ran simulations whose leaves a memo (mtaz_set_memo >= 1) can hand to another
+// batch; there ERR_ZRANGE (k_net_z's per-workgroup exponent left 0) is an error, elsewhere a note.
+static int check_err(mtaz_engine* h, bool memo_path = true) {
   int32_t e = 0;
   HIPCHK(hipMemcpyAsync(&e, h->d.pr.err, 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   if (e) {
     HIPCHK(hipMemsetAsync(h->d.pr.err, 0, 4, h->stream));
+    if ((e & ERR_ZRANGE) && !(memo_path && h->d.pr.memo >= 1)) e &= ~ERR_ZRANGE;
+    if (!e) return 0;
     std::string m;
     if (e & ERR_NODES) m += " node-capacity";
     if (e & ERR_EDGES) m += " edge-capacity";
@@ -883,6 +904,9 @@ static int check_err(mtaz_engine* h) {
     if (e & ERR_HIST) m += " history-capacity";
     if (e & ERR_HASH) m += " hash-full";
     if (e & ERR_F16) m += " activation-exceeds-f16-range";
+    if (e & ERR_ZRANGE)
+      m += " f16f8-range-with-memo (k_net_z keeps one exponent per workgroup: past 2^14 its results depend"
+           " on the batch, so memo >= 1 would hand them to other games; use f16x3 or mtaz_set_memo(0))";
     return set_err((e & ERR_ILLEGAL) ? MTAZ_E_ILLEGAL : MTAZ_E_CAPACITY, "device error flags 0x%x:%s", e, m.c_str());
   }
   return 0;
@@ -1283,19 +1307,20 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
       launch_net_f16x3_stamped(h->d, h->w, pos, n, logits, values, st, h->stream, h->variant);
     HIPCHK(hipMemcpyAsync(stamps_out, st, (size_t)nwg * NST * 8, hipMemcpyDeviceToHost, h->stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipFree(logits);
   (void)hipFree(values);
   (void)hipFree(st);
-  return check_err(h);
+  return check_err(h, false);
 }
 
 // Variants a product library accepts: each parity-green against the reference fixtures
 // (tests/test_gpu_net.py).  k_net_y: 1 = 4 boards per workgroup in every round (no tail launch),
-// 2 = the class tiles without the tap skip (bit-identity reference of the skip), 3 = round 3's
-// kernel (k_net_y3, mtaz_net16_r3.hip: bit-identity reference below 2^14, A/B).  k_net_z:
+// 2 = the class tiles without the tap skip (bit-identity reference of the skip), 5 = the first
+// round-4 tail instances.  (3 = round 3's kernel, k_net_y3 in mtaz_net16_r3.hip, batch-dependent
+// past 2^14: in the diagnostic library only, VERDICT r4 #7.)  k_net_z:
 // 1 = the product kernel with 4 boards per workgroup in every round (no tail launches; bit-identity
 // reference and A/B for the tail-balanced assignment), 2097152 = unfused epilogue (bit-identity reference), 8192 = e2m3 (fp6) cross terms,
 // 25165824 = the round-2 K loop (per-step fragment addresses, global-address weights; bit-identity
@@ -1313,7 +1338,7 @@ extern "C" int mtaz_diag_select_stamps(unsigned long long* out8, int reset) {
 
 extern "C" int mtaz_set_net_variant(mtaz_engine* h, int variant) {
   bool ok = variant == 0;
-  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 2 || variant == 3 || variant == 5;
+  if (h->precision == NET_F16X3) ok = ok || variant == 1 || variant == 2 || variant == 5;
   if (h->precision == NET_F16F8)
     ok = ok || variant == 1 || variant == 2097152 || variant == 8192 || variant == 8388608 + 16777216 ||
          variant == 33554432 || variant == 8388608 + 16777216 + 33554432;
@@ -1426,6 +1451,13 @@ extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
   return 0;
 }
 
+extern "C" int mtaz_set_sync_mode(mtaz_engine* h, int mode) {
+  if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "sync mode must be 0 (stream sync) or 1 (blocking event)");
+  h->sync_mode = mode;
+  for (mtaz_engine* p : h->parts) p->sync_mode = mode;
+  return 0;
+}
+
 extern "C" int mtaz_set_host_threads(mtaz_engine* h, int n) {
   if (n < 0) return set_err(MTAZ_E_FAIL, "host thread count must be >= 0");
   h->host_threads = n ? n : default_host_threads();
@@ -1454,8 +1486,8 @@ extern "C" int mtaz_evaluate(mtaz_engine* h, const uint32_t* d_pos, int n, float
                    d_logits + (size_t)s * NUM_ACTIONS, d_values + s, nullptr, nullptr);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
-  return check_err(h);
+  HIPCHK(stream_wait(h));
+  return check_err(h, false);   // batch evaluation: no memo hands these results on
 }
 
 // ---- fine-grained search API ----------------------------------------------------------------
@@ -1475,7 +1507,7 @@ extern "C" int mtaz_set_games(mtaz_engine* h, const uint32_t* roots, const int32
   HIPCHK(hipMemcpyAsync(h->d.gm.active, act.data(), h->G, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.nhist, zero.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.outcome, zero.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   h->last_root_k.clear();   // new roots: the next mtaz_set_noise needs a fresh mtaz_move_begin or strides
   return 0;
 }
@@ -1486,7 +1518,7 @@ extern "C" int mtaz_get_games(mtaz_engine* h, uint32_t* roots, int32_t* agents, 
   if (agents) HIPCHK(hipMemcpyAsync(agents, h->d.gm.agent, h->G * 4, hipMemcpyDeviceToHost, h->stream));
   if (active) HIPCHK(hipMemcpyAsync(active, h->d.gm.active, h->G, hipMemcpyDeviceToHost, h->stream));
   if (outcome) HIPCHK(hipMemcpyAsync(outcome, h->d.gm.outcome, h->G * 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   return 0;
 }
 
@@ -1506,7 +1538,7 @@ extern "C" int mtaz_clear_trees(mtaz_engine* h, const int32_t* trees, int n) {
   launch_reset_trees(h->d, h->d_trees, n, !all.empty(), h->stream);
   if (!all.empty()) ECHK(clear_batch_memo(h));   // all tables cleared (a new play): a new batch
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   return 0;
 }
 
@@ -1534,12 +1566,12 @@ extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t
       return set_err(MTAZ_E_FAIL, "mtaz_set_noise without strides needs mtaz_move_begin first");
     js = h->last_root_k;
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   ECHK(ensure_noise(h, (size_t)std::max<int64_t>(total, 1)));
   if (total > 0) HIPCHK(hipMemcpyAsync(h->d.gm.noise, noise, total * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offsets, h->G * 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), h->G * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   return 0;
 }
 
@@ -1586,7 +1618,7 @@ extern "C" int mtaz_leaves_get(mtaz_engine* h, int32_t* count, uint32_t* pos, in
   int32_t c = 0;
   HIPCHK(hipMemcpyAsync(&c, h->d.lf.count, 4, hipMemcpyDeviceToHost, h->stream));
   launch_gather_leaf_codes(h->d, h->d_leaf_codes, h->d_leaf_k, h->stream);
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   *count = c;
   if (c > 0) {
     HIPCHK(hipMemcpyAsync(pos, h->d.lf.pos, c * sizeof(Pos), hipMemcpyDeviceToHost, h->stream));
@@ -1594,7 +1626,7 @@ extern "C" int mtaz_leaves_get(mtaz_engine* h, int32_t* count, uint32_t* pos, in
     HIPCHK(hipMemcpyAsync(k, h->d_leaf_k, c * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipMemcpyAsync(codes, h->d_leaf_codes, (size_t)c * KMAX * 2, hipMemcpyDeviceToHost, h->stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   return 0;
 }
 
@@ -1604,7 +1636,7 @@ extern "C" int mtaz_leaves_set(mtaz_engine* h, const float* P, const float* v, i
     HIPCHK(hipMemcpyAsync(h->d.lf.P, P, (size_t)count * KMAX * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d.lf.v, v, count * 4, hipMemcpyHostToDevice, h->stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   return 0;
 }
 
@@ -1620,13 +1652,13 @@ extern "C" int mtaz_leaves_result(mtaz_engine* h, float* P, float* v, int count)
   HIPCHK(hipSetDevice(h->device));
   int32_t c = 0;
   HIPCHK(hipMemcpyAsync(&c, h->d.lf.count, 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   if (count < c) return set_err(MTAZ_E_CAPACITY, "leaf batch holds %d leaves, buffer %d", c, count);
   if (c > 0) {
     HIPCHK(hipMemcpyAsync(P, h->d.lf.P, (size_t)c * KMAX * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipMemcpyAsync(v, h->d.lf.v, c * 4, hipMemcpyDeviceToHost, h->stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   return c;
 }
 
@@ -1745,7 +1777,7 @@ extern "C" int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* po
   const int64_t npool = ne - nreg;
   uint32_t q = 0;
   if (npool > 0) {   // one block of the pool (the stream is idle between moves: plain copies suffice)
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(stream_wait(h));
     HIPCHK(hipMemcpy(&q, T.pool_used, 4, hipMemcpyDeviceToHost));
     if ((uint64_t)q + (uint64_t)npool > (uint64_t)T.pool_cap)
       return set_err(MTAZ_E_CAPACITY, "%lld edges beyond the table region do not fit the edge pool (%u of %u used)",
@@ -1791,7 +1823,7 @@ extern "C" int mtaz_tree_set(mtaz_engine* h, int tree, int n, const uint32_t* po
 
 extern "C" int mtaz_set_edge_capacity(mtaz_engine* h, int64_t per_tree, int64_t pool) {
   HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(stream_wait(h));
   for (mtaz_engine* p : h->parts) delete p;   // groups re-create their engines with the default
   h->parts.clear();
   ECHK(alloc_edges(h, per_tree, pool));
@@ -1831,6 +1863,7 @@ static int play_groups(mtaz_engine* h) {
     p->variant = h->variant;
     p->timing = h->timing;
     p->host_threads = std::max(1, h->host_threads / ng);   // the groups share this engine's threads
+    p->sync_mode = h->sync_mode;
     p->memo = h->memo;
     ECHK(ensure_batch_memo(p));
     sync_memo(p);

@@ -772,17 +772,19 @@ static int device_cus_y() {
 
 // variant 0: the product (full rounds of 4 boards, then the tail launch); 1: 4 boards per
 // workgroup throughout (no tail); 2: class tiles without the tap skip, 4 boards throughout;
-// 3: round 3's kernel (mtaz_net16_r3.hip, main + tail); 5: the product with the first round-4
+// 3: round 3's kernel (mtaz_net16_r3.hip, main + tail; diagnostic library only); 5: the product with the first round-4
 // build's tail instances (VAR bit 2: off-board cells on the padding squares, 2-way bank conflicts;
 // weights one k-block ahead)
 void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const int32_t* count, int max_b, int mode,
                       float* logits_out, float* values_out, hipStream_t s, hipEvent_t ev_begin, hipEvent_t ev_end,
                       int variant) {
   if (max_b <= 0) return;
-  if (variant == 3) {
+#ifdef MTAZ_NET_DIAG
+  if (variant == 3) {   // round 3's kernel: diagnostic library only
     launch_net_f16x3_r3(d, w, pos, count, max_b, mode, logits_out, values_out, s, ev_begin, ev_end, 0);
     return;
   }
+#endif
   if (ev_begin) (void)hipEventRecord(ev_begin, s);
   const int ncu = device_cus_y();
   const dim3 all((max_b + XB - 1) / XB);

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
 
   // dynamic range (k_net_y): the image holds x * 2^-xs, one xs per workgroup (0 for any ordinary
   // net).  mxb[bb] = max of board bb's current image, measured by the epilogue that stored it.
-  int xs = 0;
+  int xs = 0, zrange = 0;   // zrange: some layer's exponent left 0 (ERR_ZRANGE)
   float mxb[XB], mxblk[XB];
 #pragma unroll
   for (int bb = 0; bb < XB; ++bb) mxb[bb] = W.yrange[2 * CONV_LAYERS + 2], mxblk[bb] = 0.f;
@@ -251,6 +251,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
     }
     if (tid < XB) mxs[(slot ^ 1) * XB + tid] = 0u;   // every wave read them before this epilogue's barrier
     xs = xo;
+    zrange |= xo;
     __syncthreads();
 #pragma unroll
     for (int bb = 0; bb < XB; ++bb) {
@@ -983,6 +984,7 @@ __global__ __launch_bounds__(64 * ZCfg<VAR>::NW, 1) void k_net_z(Dev D, NetWeigh
 #undef Z_LOAD_B16
 #undef Z_LOAD_B8
   if (overflow && !DIAG_L2 && !DIAG_L1 && !DIAG_NOB && !DIAG_NOLDS) atomicOr(D.pr.err, ERR_F16);
+  if (zrange && tid == 0 && !DIAG_L2 && !DIAG_L1 && !DIAG_NOB && !DIAG_NOLDS) atomicOr(D.pr.err, ERR_ZRANGE);
 
   heads_reduce<NT, !W3, true>(smem, pos, b0, nb, W, tid, __builtin_ldexpf(1.f, xs),
                          make_float4(__builtin_ldexpf(1.f, -(sh[0] + 11)), __builtin_ldexpf(1.f, -(sh[1] + 11)),

@@ -99,23 +99,24 @@ class Engine:
         """'f16x3' (default, k_net_y: fp16 hi/lo split, three f16 MFMA passes, fp32-accurate to ~1e-7;
         within 1e-5 of the reference on every tested net), 'f16f8' (k_net_z: the split's cross
         terms on the block-scaled e4m3 MFMA, 1.4x faster; within 1e-5 on the seed-0 and C3 nets,
-        NOT on the round-3 stress net: tests/test_gpu_stress.py) or 'fp32' (fp32 MFMA)."""
+        NOT on the round-3 stress net: tests/test_gpu_stress.py; one exponent per workgroup, so past
+        2^14 a play with the memo on fails with 'f16f8-range-with-memo') or 'fp32' (fp32 MFMA)."""
         _lib.check(self.L.mtaz_set_precision(self.h, {'fp32': 0, 'f16x3': 1, 'f16f8': 2}[precision]))
 
     def set_net_variant(self, variant):
         """Select a parity-tested build of the current precision's network kernel (0 = product;
         set_precision resets it).  f16x3 (k_net_y): 1 = 4 boards per workgroup in every round (no
         tail launch), 2 = the class tiles without the off-board tap skip, both bitwise equal to 0;
-        3 = round 3's kernel (one stored-units exponent per workgroup; bitwise equal to 0 on nets
-        whose activations stay below 2^14), 5 = the product with the first round-4 tail instances
+        5 = the product with the first round-4 tail instances
         (off-board cells on the padding squares, 2-way LDS bank conflicts; weights one k-block
         ahead; bitwise equal to 0).  f16f8 (k_net_z): 1 = 4 boards per workgroup in every
         round (no tail launches), 2097152 = the epilogue in unfused form, 8192 = e2m3 (fp6) cross
         terms, 25165824 = the round-2 K loop (per-step fragment addresses, 64-bit weight addresses),
         33554432 = the round-2 epilogue (unscaled conversions), 58720256 = both (the round-2
         product); all but 8192 bitwise equal to 0.  Other values are rejected; the A/B and
-        timing-only diagnostic builds exist only in libmtaz_diag.so (MTAZ_LIB, tools/bench_net.py
-        --diag)."""
+        timing-only diagnostic builds, and round 3's k_net_y (f16x3 variant 3: one stored-units
+        exponent per workgroup, batch-dependent past 2^14), exist only in libmtaz_diag.so
+        (MTAZ_LIB, tools/bench_net.py --diag, tests/diag_round3.py)."""
         _lib.check(self.L.mtaz_set_net_variant(self.h, int(variant)))
 
     def set_pipeline(self, groups):
@@ -141,6 +142,11 @@ class Engine:
     def set_host_threads(self, n=0):
         """Host threads of the per-move work (0 = the process's affinity mask, at most 16)."""
         _lib.check(self.L.mtaz_set_host_threads(self.h, int(n)))
+
+    def set_sync_mode(self, mode=0):
+        """How the host thread waits for the engine's stream: 0 = hipStreamSynchronize (default),
+        1 = a blocking-sync event (the thread sleeps instead of holding a CPU).  Results unchanged."""
+        _lib.check(self.L.mtaz_set_sync_mode(self.h, int(mode)))
 
     def set_seed_base(self, seed_base):
         """Game slot g of the next play() uses np.random.seed(seed_base + g) semantics."""

@@ -73,19 +73,29 @@ def gather_records(rec, dist, dst=0):
     return [EpisodeRecords(o['pos'], o['k'], o['codes'], o['visits'], o['reward']) for o in out]
 
 
-def arena_round(new_net, old_net, games, sims, dist, device, seed_base):
+def arena_verdict(res, dist, device, gate_threshold):
+    """This rank's arena counts summed over every rank (one all_reduce), the score of
+    exp/learner.py:97-145 (new wins / decisive games) and the 0.55 gate of app/base.py:194-196:
+    every rank reaches the same verdict from the same sums, so all keep or all revert."""
+    cnt = torch.tensor([res['new_wins'], res['old_wins'], res['draws'], res['games']], dtype=torch.float64,
+                       device=device)
+    if dist is not None:
+        dist.all_reduce(cnt)
+    nw, ow, dr, ng = cnt.tolist()
+    score = nw / (nw + ow + 1e-8)
+    return {'new_wins': int(nw), 'old_wins': int(ow), 'draws': int(dr), 'games': int(ng), 'score': score,
+            'accepted': score > gate_threshold}
+
+
+def arena_round(new_net, old_net, games, sims, dist, device, seed_base, gate_threshold=0.55):
     """Sharded arena: each rank plays `games` games per side; counts summed over ranks."""
     from .arena import arena
     from .engine import Engine
     eng = Engine(n_games=games, sims=sims, device=device)
     res = arena(eng, new_net, old_net, seed_base=seed_base)
-    cnt = torch.tensor([res['new_wins'], res['old_wins'], res['draws'], res['games']], dtype=torch.float64,
-                       device=torch.device('cuda', device))
-    if dist is not None:
-        dist.all_reduce(cnt)
-    nw, ow, dr, ng = cnt.tolist()
-    return {'new_wins': int(nw), 'old_wins': int(ow), 'draws': int(dr), 'games': int(ng),
-            'score': nw / (nw + ow + 1e-8)}
+    eng.close()
+    dev = torch.device('cuda', device) if dist is None or dist.get_backend() != 'gloo' else torch.device('cpu')
+    return arena_verdict(res, dist, dev, gate_threshold)
 
 
 def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None, device=0, seed=0,
@@ -140,8 +150,8 @@ def run_loop(iterations, games, sims, batch_size=32, epochs=1, lr=0.2, dist=None
             prev = Network()
             prev.load_state_dict(old_sd)
             verdict = arena_round(net, prev, arena_games, sims, dist, device,
-                                  seed_base=10 ** 9 + (it * world + rank) * 2 * arena_games)
-            verdict['accepted'] = verdict['score'] > gate_threshold
+                                  seed_base=10 ** 9 + (it * world + rank) * 2 * arena_games,
+                                  gate_threshold=gate_threshold)
             if not verdict['accepted']:
                 net.load_state_dict(old_sd)
                 if rank == 0:

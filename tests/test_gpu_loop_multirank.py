@@ -46,3 +46,34 @@ def test_loop_ranks_equal_one_process(tmp_path, world):
         assert a['loss'] == b['loss'], (a['loss'], b['loss'])
     assert res['head'] == flat[:2000].tolist() and res['tail'] == flat[-2000:].tolist()
     assert res['sum'] == flat.double().sum().item()
+
+
+@pytest.mark.parametrize('gate', [2.0, -1.0])
+def test_loop_arena_gating_two_ranks(tmp_path, gate):
+    """C5 with gating (arena_games > 0) at world 2: both ranks play their arena shard,
+    the counts are all-reduced, and both keep or revert alike.  gate 2.0 can never pass (score <= 1):
+    every update is reverted, so both ranks end on the initial weights (torch.manual_seed(0);
+    Network()) bitwise.  gate -1.0 always passes: both ranks end on the same trained weights, which
+    differ from the initial ones."""
+    import torch
+    from minitchess_alphazero_amd.launch import spawn_ranks
+    from minitchess_alphazero_amd.loop import flat_weights
+    from minitchess_alphazero_amd.network import Network
+    G, sims, iters, arena_games = 4, 4, 2, 2
+    out = str(tmp_path / 'loop.json')
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    rc = spawn_ranks(2, [sys.executable, os.path.join(REPO, 'tests', 'rank_worker_loop.py'), out, str(G), str(sims),
+                         str(iters), str(arena_games), str(gate)], env=env)
+    assert rc == 0
+    res = json.load(open(out))
+    r0, r1 = (json.load(open(f'{out}.rank{r}')) for r in (0, 1))
+    assert r0 == r1                                   # same weights on both ranks, bitwise
+    assert len(res['history']) == iters
+    for h in res['history']:
+        a = h['arena']
+        assert a['games'] == 2 * 2 * arena_games      # both ranks' games, both sides
+        assert a['accepted'] == (gate < 0)
+    torch.manual_seed(0)
+    init, _ = flat_weights(Network(), 'cpu')
+    same_as_init = r0['head'] == init[:2000].tolist() and r0['tail'] == init[-2000:].tolist()
+    assert same_as_init == (gate > 1)

@@ -148,6 +148,21 @@ def test_edge_pool_spill_and_exhaustion():
     small.set_edge_capacity(64, 256)
     with pytest.raises(_lib.MtazError, match='edge-capacity'):
         small.play()
+    # the state the round-4 fault (r04s) left behind.  After the capacity
+    # error the same engine, given its pool back, plays the same games bit-exactly, and a new
+    # engine on the same device works: the error is reported and cleared, the context is sound.
+    small.set_edge_capacity(64, 1 << 21)
+    st2 = small.play()
+    r2 = small.records()
+    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+        assert np.array_equal(r2[key], r_ref[key]), key
+    assert st2['games'] == st_ref['games'] and st2['plies'] == st_ref['plies']
+    fresh = _engine(16, 16, seed_base=3)
+    fresh.set_weights(net)
+    fresh.play()
+    r3 = fresh.records()
+    for key in ('plies', 'pos', 'action', 'visits', 'reward'):
+        assert np.array_equal(r3[key], r_ref[key]), key
 
 
 def test_numpy1_cast_mode_vs_oracle():

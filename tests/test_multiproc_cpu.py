@@ -124,3 +124,50 @@ def test_loop_exchange_ranks(world):
     assert [p[1] for p in parts] == [res[r][3] for r in range(world)]
     assert all(res[r][1] is None for r in range(1, world))
     assert all(res[0][4] == res[r][4] and res[0][5] == res[r][5] for r in range(world))   # identical weights
+
+
+def _arena_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import torch.distributed as dist
+    from minitchess_alphazero_amd.loop import arena_verdict
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank, world_size=world)
+    # rank-local arena counts whose LOCAL verdicts disagree: rank 0 alone would keep the new net
+    # (3 of 3 decisive games), every other rank alone would revert (0 of 2)
+    local = ({'new_wins': 3, 'old_wins': 0, 'draws': 1, 'games': 4} if rank == 0 else
+             {'new_wins': 0, 'old_wins': 2, 'draws': 2, 'games': 4})
+    out = {th: arena_verdict(local, dist, torch.device('cpu'), th) for th in (0.55, 0.5, 0.3)}
+    gathered = [None] * world
+    dist.all_gather_object(gathered, out)
+    if rank == 0:
+        q.put(gathered)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 8])
+def test_arena_gate_same_verdict_on_every_rank(world):
+    """C5 gating at world > 1 (loop.run_loop with arena_games > 0): the ranks' arena
+    counts are all-reduced and every rank applies the 0.55 gate (app/base.py:194-196) to the same
+    sums, so all keep or all revert even when a rank's own games point the other way."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_arena_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nw, ow = 3, 2 * (world - 1)
+    for th in (0.55, 0.5, 0.3):
+        verdicts = [g[th] for g in gathered]
+        assert all(v == verdicts[0] for v in verdicts), th
+        v = verdicts[0]
+        assert (v['new_wins'], v['old_wins'], v['games']) == (nw, ow, 4 * world)
+        assert v['accepted'] == (nw / (nw + ow + 1e-8) > th)
+    # the thresholds split the outcomes: at world 2 (score 0.6) 0.55 keeps, at world 8 (score 0.18) it reverts
+    assert gathered[0][0.55]['accepted'] == (world == 2)
+    assert gathered[0][0.3]['accepted'] == (world == 2)

@@ -80,7 +80,7 @@ for step in "$@"; do
         run "pmcnet $i" "${PMC_TIMEOUT:-300}" rocprofv3 --pmc $grp --kernel-include-regex "k_net_y" \
           -d "$OUT/pmcnet${PMCNET_TAG}/p$i" -o pmc --output-format csv -- python3 tools/bench_net.py --variants ${PMCNET_VARIANTS:-f16x3:0} \
           --rounds 1 --iters 5 > "$OUT/pmcnet${PMCNET_TAG}_p$i.log" 2>&1
-        rc=$?; tail -1 "$OUT/pmcnet_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
+        rc=$?; tail -1 "$OUT/pmcnet${PMCNET_TAG}_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
     pmci)
       run pmci "${PMC_TIMEOUT:-420}" rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD \

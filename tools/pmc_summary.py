@@ -52,6 +52,17 @@ def bench_config(root):
     return None, None, None
 
 
+def bench_hashes(root):
+    """The mtaz_src_sha256 of every bench line under `root` (one per PMC pass)."""
+    out = set()
+    logs = glob.glob(os.path.join(root, 'p*.log')) + glob.glob(os.path.join(os.path.dirname(root.rstrip('/')), 'pmc_p*.log'))
+    for log in logs:
+        for ln in open(log):
+            if ln.startswith('{') and '"mtaz_src_sha256"' in ln:
+                out.add(json.loads(ln)['mtaz_src_sha256'])
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('root')
@@ -89,6 +100,11 @@ def main():
     }
     if line is not None:
         out['boards_per_launch'] = line['roofline']['flop_per_launch'] / 638245892
+        # the library the passes ran (bench.py attaches this file's traffic only to a run of the same one)
+        out['mtaz_src_sha256'] = line.get('mtaz_src_sha256')
+    hashes = bench_hashes(args.root)
+    if len(hashes) > 1:
+        raise SystemExit(f'PMC passes ran different libraries: {sorted(hashes)}')
     json.dump(out, open(args.out, 'w'), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -36,6 +36,7 @@ import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -59,6 +60,10 @@ def measure(net, rec, device, max_pos=2048):
         h.remove()
     logits = logits.double().cpu().numpy()
     value = value.double().cpu().numpy().reshape(-1)
+    # round 5: k_net_y's per-board stored-units exponents on these positions (tools/net_range.py)
+    from net_range import xs_profile
+    prof = xs_profile(net.state_dict(), tok, clk, device=device)
+    xs = prof['xs']
     spreads, pmax = [], []
     for j, i in enumerate(idx):
         codes = rec.codes[starts[i]:starts[i] + rec.k[i]].astype(np.int64)
@@ -68,7 +73,9 @@ def measure(net, rec, device, max_pos=2048):
         pmax.append(float((e / e.sum()).max()))
     return {'trunk_max': max(acts), 'spread_max': float(np.max(spreads)), 'spread_med': float(np.median(spreads)),
             'pmax_med': float(np.median(pmax)), 'value_std': float(value.std()), 'value_min': float(value.min()),
-            'value_max': float(value.max()), 'logit_absmax': float(np.abs(logits).max()), 'positions': int(n)}
+            'value_max': float(value.max()), 'logit_absmax': float(np.abs(logits).max()), 'positions': int(n),
+            'logits_finite': bool(np.isfinite(logits).all() and np.isfinite(value).all()),
+            'xs_max': int(xs.max()), 'xs_boards': int((xs > 0).any(0).sum()), 'xs_layers': [int(v) for v in xs.max(1)]}
 
 
 FILES, RANKS = 5, 6
@@ -190,6 +197,11 @@ def main():
     ap.add_argument('--endgame-frac', type=float, default=0.0,
                     help='round 4: fraction of each iteration\'s games started from random endgame starts '
                          '(endgame_fen) instead of STARTING_FEN')
+    ap.add_argument('--min-xs', type=int, default=0,
+                    help='round 5: also require k_net_y\'s per-board exponent >= this on some position '
+                         '(tools/net_range.py; 1 = the bound passes 2^14)')
+    ap.add_argument('--min-xs-boards', type=int, default=1,
+                    help='round 5: ... on at least this many of the measured positions')
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--fallback-best', action='store_true',
                     help='if no iteration qualifies, save the one past the other criteria with the largest '
@@ -220,7 +232,9 @@ def main():
             m['decisive_frac'] = h.get('decisive_frac')
             base_ok = (it >= args.min_iteration and m['trunk_max'] >= args.min_trunk
                        and m['spread_max'] >= args.min_spread and m['logit_absmax'] <= args.max_logit)
-            m['qualifies'] = base_ok and m['value_std'] >= args.min_value_std
+            m['qualifies'] = (base_ok and m['value_std'] >= args.min_value_std and m['logits_finite']
+                              and (args.min_xs <= 0 or (m['xs_max'] >= args.min_xs
+                                                        and m['xs_boards'] >= args.min_xs_boards)))
             # --fallback-best: the network past the other criteria with the largest value_std, kept in
             # case no iteration reaches --min-value-std
             if args.fallback_best and base_ok and m['value_std'] > best[lr][0]:
@@ -260,7 +274,8 @@ def main():
            'sims': args.sims, 'endgame_frac': args.endgame_frac, 'seed': args.seed, 'fallback_pick': fallback,
            'criteria': {'min_iteration': args.min_iteration, 'min_trunk': args.min_trunk,
                         'min_spread': args.min_spread, 'max_logit': args.max_logit,
-                        'min_value_std': args.min_value_std}}
+                        'min_value_std': args.min_value_std, 'min_xs': args.min_xs,
+                        'min_xs_boards': args.min_xs_boards}}
     if pick is not None and args.save:
         from safetensors.torch import save_file
         os.makedirs(os.path.dirname(os.path.abspath(args.save)), exist_ok=True)
