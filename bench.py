@@ -276,9 +276,11 @@ def main():
                          '(launch.rank_host_share: usable CPUs / N): before anything touches the GPU, pin '
                          'to that many cores of the affinity mask and use that many host threads '
                          '(VERDICT r4 #2: the 8-rank host share measured on a 1-GPU box)')
-    ap.add_argument('--sync-mode', type=int, default=0, choices=[0, 1],
+    ap.add_argument('--sync-mode', type=int, default=-1, choices=[-1, 0, 1],
                     help='how the engine waits for its stream: 0 = hipStreamSynchronize, 1 = blocking-sync '
-                         'event (Engine.set_sync_mode)')
+                         'event (Engine.set_sync_mode); -1 (default) = 1 when this rank has a share of a '
+                         'multi-rank node (N > 1 or --rank-share), else 0 (profiles/r05/hostshare: +2.1%% '
+                         'at the 2-CPU share, neutral at 16)')
     ap.add_argument('--one-thread-during-warmup', type=int, default=1, choices=[0, 1],
                     help='1 (default): run the CPU baseline 1-thread legs during engine setup and the '
                          'untimed warm-up steps (collected before the timed region); 0: after the timed '
@@ -370,7 +372,8 @@ def main():
     eng.set_net_variant(args.net_variant)
     eng.set_timing(True)
     eng.set_pipeline(args.groups)
-    eng.set_sync_mode(args.sync_mode)
+    sync_mode = args.sync_mode if args.sync_mode >= 0 else int(world > 1 or rank_share is not None)
+    eng.set_sync_mode(sync_mode)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
     LEG_HOST_THREADS = 2
     if legs is not None:
@@ -493,6 +496,7 @@ def main():
         eng36.set_pipeline(args.groups)
         eng36.set_memo(args.memo)
         eng36.set_host_threads(eng_threads)
+        eng36.set_sync_mode(sync_mode)
         eng36.evaluate(np.stack([start_position()] * 8))
         dt3, tot3, prec3 = timed(eng36, 1, f'{args.default_sims} sims')
         at_default = {'sims_per_move': args.default_sims, 'value': G * world / dt3, 'unit': 'games/s', 'steps': 1,
@@ -588,7 +592,7 @@ def main():
         # CPUs it keeps busy on average, against its share of the node (launch.rank_host_share)
         'host_cpu_s': tot['host_cpu_ms'] / 1e3 / world,
         'host_cpus_busy': tot['host_cpu_ms'] / 1e3 / world / dt,
-        'sync_mode': args.sync_mode,
+        'sync_mode': sync_mode,
         'mtaz_src_sha256': lib_hash,
     }
     if rank_share is not None:

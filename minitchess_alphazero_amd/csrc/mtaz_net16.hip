@@ -224,6 +224,11 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   constexpr bool TAIL_R3 = (VAR & 2) != 0;   // tails as first built in round 4 (per-board tiles, zero cells, ring)
   constexpr bool CLS3 = NVB == 3 && !TAIL_R3;  // the 3-board instance on class tiles (round 4b)
   constexpr bool SKIP = (NVB == XB || CLS3) && (VAR & 1) == 0;
+  // diagnostic forms (libmtaz_diag.so only; wrong results by construction, for timing and the
+  // clock under the power limit): 8 = no weight loads in the conv K loops (the ring
+  // keeps the layer prologue's fragments), 16 = no activation fragment reads in the K loops (the
+  // MFMAs reuse the layer's first fragments), 32 = no epilogue image stores
+  constexpr bool D_NOW = (VAR & 8) != 0, D_NOF = (VAR & 16) != 0, D_NOE = (VAR & 32) != 0;
   int b0, nb;
   {   // tail-balanced board assignment (round 3): full rounds of 4 boards, then 1-3 per CU
     const int n = count ? *count : max_b;
@@ -358,8 +363,10 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
 #pragma unroll
         for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
         const uint2 hp = __builtin_bit_cast(uint2, yh);
-        *reinterpret_cast<uint2*>(smem + ah) = hp;
-        *reinterpret_cast<uint2*>(smem + al) = make_uint2(ny_lo_pair(hp.x, y[0], y[1]), ny_lo_pair(hp.y, y[2], y[3]));
+        if constexpr (!D_NOE) {
+          *reinterpret_cast<uint2*>(smem + ah) = hp;
+          *reinterpret_cast<uint2*>(smem + al) = make_uint2(ny_lo_pair(hp.x, y[0], y[1]), ny_lo_pair(hp.y, y[2], y[3]));
+        }
       }
     }
     // per-board max of the new image (y >= 0: float bits order as values; NaN above +inf), each
@@ -601,14 +608,15 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
                   if (nd[i] && c++ == Q / 2) return i;
                 return 0;
               }();
-              BN[(Q & 1) * 4 + I] = *reinterpret_cast<const f16x8*>(smem + o[I] + 1024 * (U1 & 7) + (Q & 1) * PART_B);
+              if constexpr (!D_NOF)
+                BN[(Q & 1) * 4 + I] = *reinterpret_cast<const f16x8*>(smem + o[I] + 1024 * (U1 & 7) + (Q & 1) * PART_B);
             } else if constexpr (Q == NFR) {   // the table entries of (U2, H2)
               const int ta = U2 < 24 ? tab_j + (U2 / 8) * 2048 + H2 * 1024 : tab_n + ((U2 - 24) / 8) * 2048 + H2 * 1024;
               tpre = *reinterpret_cast<const uint4*>(smem + ta);
             } else {                           // weight load: k-block U + PD, channel tile / part
               constexpr int W_ = Q - NFR - 1, ct = W_ >> 1, part = W_ & 1;
               const int kbn = kb_j + U + PD < KBY ? kb_j + U + PD : KBY - 1;   // (clamped: the layer's last k-blocks)
-              wload(AN[2 * ct + part], kbn, ct, part);
+              if constexpr (!D_NOW) wload(AN[2 * ct + part], kbn, ct, part);
             }
           });
           sfor<a0, a1>([&](auto a_c) __attribute__((always_inline)) {
@@ -801,6 +809,16 @@ void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const i
   } else if (variant == 2) {
     hipLaunchKernelGGL((k_net_y<false, 1, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, 0);
+#ifdef MTAZ_NET_DIAG
+  } else if (variant == 8 || variant == 16 || variant == 24 || variant == 32 || variant == 56) {
+    // the diagnostic forms, 4 boards per workgroup throughout (tools/bench_net.py --diag)
+#define Y_DIAG(V)                                                                                                  \
+  if (variant == V)                                                                                                \
+    hipLaunchKernelGGL((k_net_y<false, V, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out, \
+                       values_out, nullptr, 0);
+    Y_DIAG(8) Y_DIAG(16) Y_DIAG(24) Y_DIAG(32) Y_DIAG(56)
+#undef Y_DIAG
+#endif
   } else {
     hipLaunchKernelGGL((k_net_y<false, 0, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, 0);
@@ -815,6 +833,13 @@ void launch_net_f16x3_stamped(const Dev& d, const NetWeights& w, const Pos* pos,
   if (variant == 2)
     hipLaunchKernelGGL((k_net_y<true, 1, XB>), all, dim3(256), 0, s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS,
                        logits_out, values_out, stamps, 0);
+#ifdef MTAZ_NET_DIAG
+#define Y_DIAG(V)                                                                                               \
+  else if (variant == V) hipLaunchKernelGGL((k_net_y<true, V, XB>), all, dim3(256), 0, s, d, w, pos, nullptr, n, \
+                                            (int)NET_FULL_LOGITS, logits_out, values_out, stamps, 0);
+  Y_DIAG(8) Y_DIAG(16) Y_DIAG(24) Y_DIAG(32) Y_DIAG(56)
+#undef Y_DIAG
+#endif
   else
     hipLaunchKernelGGL((k_net_y<true, 0, XB>), all, dim3(256), 0, s, d, w, pos, nullptr, n, (int)NET_FULL_LOGITS,
                        logits_out, values_out, stamps, 0);

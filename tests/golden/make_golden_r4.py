@@ -6,10 +6,16 @@ VERDICT r3 #3: the round-3 stress checkpoint's value head collapsed to a constan
 data was almost all draws), so every value check on it passed trivially.  tools/train_stress.py
 --endgame-frac 0.5 trained stress4 in the C5 loop with half of each iteration's games started from
 random K + heavy pieces v K positions, which end decisively often enough for the value targets to
-vary, and kept the first network past 20 updates with trunk activations >= 2^14 (so k_net_y's
-stored-units exponents leave 0: VERDICT r3 #2), peaked priors and value_std >= 0.1.  The checkpoint
-is data (GPU training is not bitwise reproducible); this script pins it and records what the
-reference computes on it:
+vary, at lr 0.003, and kept the first network past 20 updates that met the criteria the training
+log records: trunk |activation| >= 100 (min_trunk), legal-logit spread >= 8 (min_spread), largest
+|logit| <= 3000 and value_std >= 0.05 (iteration 19 of its run: trunk 169, value_std 0.054).  On
+the fixture positions below the reference measures trunk |activation| up to 190.6, legal-logit
+spreads up to 5.8 (median 0.75), a median top prior of 0.23 and values -0.26 .. 0.33 (std 0.058):
+a value head that varies, but NOT the range past 2^14 where k_net_y's per-board stored-units
+exponents leave 0 (tools/net_range.py: 0 on every layer and position).  That path is pinned by the
+round-3 'stress' net (lightly: one position) and the wide-range test net, and, with varying values,
+by round 5's stress5 (make_golden_r5.py).  The checkpoint is data (GPU training is not bitwise
+reproducible); this script pins it and records what the reference computes on it:
 
   stress4.json       sha256 of the checkpoint (oracle.net.state_dict_sha256), the training log
                      (tools/train_stress.py output), the network's ranges on the fixture positions

@@ -16,6 +16,7 @@
 #   pmc              rocprofv3 --pmc passes on the network kernel, one counter group per pass
 #                    (FETCH_SIZE / WRITE_SIZE / TCC hit-miss / SQ busy group), of bench.py $PMC_ARGS;
 #                    summarise with python tools/pmc_summary.py gpurun_out/OUT/pmc
+#   pmcdiag          one PMC pass (MFMA busy, cycles, GRBM) over k_net_y's product + diagnostic forms
 #   pmci             the instruction-mix PMC pass (SQ_INSTS_*) of bench.py $PMC_ARGS
 #   ab               tools/bench_net.py A/B of network variants $AB_VARIANTS (AB_DIAG=1: diagnostic library)
 #   netab            the same on the product library for the variants it accepts
@@ -82,6 +83,14 @@ for step in "$@"; do
           --rounds 1 --iters 5 > "$OUT/pmcnet${PMCNET_TAG}_p$i.log" 2>&1
         rc=$?; tail -1 "$OUT/pmcnet${PMCNET_TAG}_p$i.log"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
+    pmcdiag)
+      # one PMC pass (MFMA busy, wave and busy cycles, GPU-active clocks) over the network kernel's
+      # product and diagnostic forms in one process (tools/bench_net.py --diag $PMCDIAG_VARIANTS)
+      run pmcdiag "${PMC_TIMEOUT:-300}" rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex "k_net_y" \
+        -d "$OUT/pmcdiag" -o pmc --output-format csv -- python3 tools/bench_net.py --diag \
+        --variants ${PMCDIAG_VARIANTS:-f16x3:0} --rounds 1 --iters 5 > "$OUT/pmcdiag.log" 2>&1
+      rc=$?; tail -1 "$OUT/pmcdiag.log"; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     pmci)
       run pmci "${PMC_TIMEOUT:-420}" rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
         SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE --kernel-include-regex "k_net_[yz]" \
