@@ -148,8 +148,11 @@ int mtaz_set_host_threads(mtaz_engine* h, int n);
  * bench.py --sync-mode, --rank-share).  Results are identical in both modes. */
 int mtaz_set_sync_mode(mtaz_engine* h, int mode);
 /* network-only timing harness: avg ms over `iters` launches on n device positions; with
- * stamped != 0 also per-workgroup [nwg][stem, conv K loops, epilogues, heads cycles, total
- * cycles, total 100 MHz ticks] from a separate diagnostic build (tools/bench_net.py) */
+ * stamped != 0 also, from one more launch of the stamp-instrumented build (4 boards per
+ * workgroup, nwg = ceil(n / 4)), stamps_out[nwg * 10]: per workgroup [nwg][stem, conv K loops,
+ * epilogues, heads cycles, total cycles, total 100 MHz ticks], then (k_net_y) per board
+ * [nwg][4]: (largest stored-units exponent << 32) | bit mask of the layers whose exponent is
+ * nonzero (bit 0 = stem, 1 + L = conv L) (tools/bench_net.py, tests/test_gpu_stress.py) */
 int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int iters, int stamped, float* ms_out,
                   uint64_t* stamps_out);
 /* select a network kernel code variant of the current precision for A/B timing (0 = the

@@ -1283,10 +1283,11 @@ extern "C" int mtaz_net_time(mtaz_engine* h, const uint32_t* d_pos, int n, int i
   float *logits = nullptr, *values = nullptr;
   unsigned long long* st = nullptr;
   const int nwg = (n + 3) / 4;
-  const int NST = 6;
+  const int NST = 10;   // per workgroup: 6 phase stamps, then (in a second region) 4 exponent records
   HIPCHK(hipMalloc(&logits, (size_t)n * NUM_ACTIONS * 4));
   HIPCHK(hipMalloc(&values, (size_t)n * 4));
   HIPCHK(hipMalloc(&st, (size_t)nwg * NST * 8));
+  HIPCHK(hipMemset(st, 0, (size_t)nwg * NST * 8));
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));

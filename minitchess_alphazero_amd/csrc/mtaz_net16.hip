@@ -225,9 +225,11 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   constexpr bool CLS3 = NVB == 3 && !TAIL_R3;  // the 3-board instance on class tiles (round 4b)
   constexpr bool SKIP = (NVB == XB || CLS3) && (VAR & 1) == 0;
   // diagnostic forms (libmtaz_diag.so only; wrong results by construction, for timing and the
-  // clock under the power limit): 8 = no weight loads in the conv K loops (the ring
-  // keeps the layer prologue's fragments), 16 = no activation fragment reads in the K loops (the
-  // MFMAs reuse the layer's first fragments), 32 = no epilogue image stores
+  // clock under the power limit), each keeping the MFMA operands real data: 8 = no
+  // weight loads in the conv K loops (the layer prologue fills every slot of the ring with a real
+  // k-block, which the loop then reuses), 16 = no activation fragment reads in the K loops (the
+  // prologue reads both halves' fragments of the layer's first k-block), 32 = no conv epilogue
+  // image stores (the image keeps the stem's real activations)
   constexpr bool D_NOW = (VAR & 8) != 0, D_NOF = (VAR & 16) != 0, D_NOE = (VAR & 32) != 0;
   int b0, nb;
   {   // tail-balanced board assignment (round 3): full rounds of 4 boards, then 1-3 per CU
@@ -283,6 +285,19 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   // only.  xo = max(0, ilogb(bound) - 14) keeps every stored value below 2^15; the rescaling is by
   // powers of two, hence exact; an ordinary net keeps xs = 0 (and round 3's bits).
   int xs[4] = {0, 0, 0, 0};
+  // stamped build: per board, the layers whose stored-units exponent is nonzero (bit 0 = stem, bit
+  // 1 + L = conv L) and the largest exponent, written after the phase stamps (mtaz_net_time)
+  uint32_t xs_mask[4] = {0u, 0u, 0u, 0u};
+  int xs_max[4] = {0, 0, 0, 0};
+  auto note_xs = [&](int layer) {
+    if constexpr (STAMP) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        xs_mask[b] |= (uint32_t)(xs[b] != 0) << layer;
+        xs_max[b] = xs[b] > xs_max[b] ? xs[b] : xs_max[b];
+      }
+    }
+  };
   float mx_img[4], mx_blk[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int b = 0; b < 4; ++b) mx_img[b] = W.yrange[2 * CONV_LAYERS + 2];   // max |embedding|
@@ -363,7 +378,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
 #pragma unroll
         for (int j = 0; j < 4; ++j) yh[j] = (_Float16)y[j];
         const uint2 hp = __builtin_bit_cast(uint2, yh);
-        if constexpr (!D_NOE) {
+        if (!D_NOE || bias == W.stem_b) {   // (diagnostic form 32: the stem's image only)
           *reinterpret_cast<uint2*>(smem + ah) = hp;
           *reinterpret_cast<uint2*>(smem + al) = make_uint2(ny_lo_pair(hp.x, y[0], y[1]), ny_lo_pair(hp.y, y[2], y[3]));
         }
@@ -496,6 +511,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
     for (int b = 0; b < 4; ++b)
       bnd[b] = __builtin_fmaf(W.yrange[2 * CONV_LAYERS], mx_img[b], W.yrange[2 * CONV_LAYERS + 1]) * 1.0009765625f;
     epilogue(W.stemx_inv[0], W.stem_b, std::false_type{}, 0.f, bnd);
+    note_xs(0);
   }
   stamp(st_stem);
 
@@ -530,7 +546,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
   for (int L = 0; L < CONV_LAYERS; ++L) {
     // layer prologue: k-block 0's weights, half-step (0, 0)'s fragments, the offsets of (0, 1)
 #pragma unroll
-    for (int kp = 0; kp < PD; ++kp)
+    for (int kp = 0; kp < (D_NOW ? RS : PD); ++kp)
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
         wload(A[kp][2 * c], kp, c, 0);
@@ -547,6 +563,14 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
           BH[0][4 + i] = *reinterpret_cast<const f16x8*>(smem + o[i] + PART_B);
         }
       onx[0] = (int)e1.x, onx[1] = (int)e1.y, onx[2] = (int)e1.z, onx[3] = (int)e1.w;
+      if constexpr (D_NOF) {   // diagnostic: half 1's fragments too, reused by every k-block
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < NVB) {
+            BH[1][i] = *reinterpret_cast<const f16x8*>(smem + onx[i]);
+            BH[1][4 + i] = *reinterpret_cast<const f16x8*>(smem + onx[i] + PART_B);
+          }
+      }
     }
     for (int j = 0; j < 3; ++j) {   // T (half 0) runs no dr = -1 taps (j = 0), B (half 1) no dr = +1 (j = 2)
       const int tab_j = tab_l + 6144 * j;
@@ -677,9 +701,10 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
         bnd[b] = (__builtin_fmaf(W.yrange[2 * L], mx_img[b], W.yrange[2 * L + 1]) + mx_blk[b]) * 1.0009765625f;
       epilogue(W.convx_inv[L], W.conv_b + L * 256, std::false_type{}, 0.f, bnd);
     }
+    note_xs(1 + L);
     stamp(st_epi);
   }
-  if (overflow) atomicOr(D.pr.err, ERR_F16);
+  if (overflow && !D_NOW && !D_NOF && !D_NOE) atomicOr(D.pr.err, ERR_F16);   // (diagnostic forms: garbage by design)
 
   // ---------------- heads (exp/policy.py:62-69, :76-79) ------------------------------------
   {
@@ -735,6 +760,7 @@ __device__ __forceinline__ void net_y_body(char* smem, const int bid, const Dev&
       stamps[bid * 6 + 4] = __builtin_amdgcn_s_memtime() - t_start;
       stamps[bid * 6 + 5] = __builtin_amdgcn_s_memrealtime() - r_start;
     }
+    if (tid < 4) stamps[(size_t)gridDim.x * 6 + bid * 4 + tid] = ((unsigned long long)xs_max[tid] << 32) | xs_mask[tid];
   }
   heads_out<true>(D, smem, b0, nb, W, mode, logits_out, values_out, wave, lane);
 }
@@ -810,13 +836,13 @@ void launch_net_f16x3(const Dev& d, const NetWeights& w, const Pos* pos, const i
     hipLaunchKernelGGL((k_net_y<false, 1, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out,
                        values_out, nullptr, 0);
 #ifdef MTAZ_NET_DIAG
-  } else if (variant == 8 || variant == 16 || variant == 24 || variant == 32 || variant == 56) {
+  } else if (variant == 8 || variant == 16 || variant == 32) {
     // the diagnostic forms, 4 boards per workgroup throughout (tools/bench_net.py --diag)
 #define Y_DIAG(V)                                                                                                  \
   if (variant == V)                                                                                                \
     hipLaunchKernelGGL((k_net_y<false, V, XB>), all, dim3(256), 0, s, d, w, pos, count, max_b, mode, logits_out, \
                        values_out, nullptr, 0);
-    Y_DIAG(8) Y_DIAG(16) Y_DIAG(24) Y_DIAG(32) Y_DIAG(56)
+    Y_DIAG(8) Y_DIAG(16) Y_DIAG(32)
 #undef Y_DIAG
 #endif
   } else {
@@ -837,7 +863,7 @@ void launch_net_f16x3_stamped(const Dev& d, const NetWeights& w, const Pos* pos,
 #define Y_DIAG(V)                                                                                               \
   else if (variant == V) hipLaunchKernelGGL((k_net_y<true, V, XB>), all, dim3(256), 0, s, d, w, pos, nullptr, n, \
                                             (int)NET_FULL_LOGITS, logits_out, values_out, stamps, 0);
-  Y_DIAG(8) Y_DIAG(16) Y_DIAG(24) Y_DIAG(32) Y_DIAG(56)
+  Y_DIAG(8) Y_DIAG(16) Y_DIAG(32)
 #undef Y_DIAG
 #endif
   else

@@ -94,6 +94,23 @@ class Engine:
                                         c_void_p(values.data_ptr())))
         return logits.cpu().numpy(), values.cpu().numpy()
 
+    def net_exponents(self, positions):
+        """k_net_y's stored-units exponents on packed positions [n,5], from one launch of the
+        stamp-instrumented build (mtaz_net_time, 4 boards per workgroup): (largest exponent [n],
+        bit mask of the layers whose exponent is nonzero [n]; bit 0 = stem, 1 + L = conv L)."""
+        import torch
+        dev = torch.device('cuda', self.device)
+        pos = torch.from_numpy(np.ascontiguousarray(positions, np.uint32).view(np.int32)).to(dev)
+        n = pos.shape[0]
+        nwg = (n + 3) // 4
+        st = np.zeros(nwg * 10, np.uint64)
+        ms = ctypes.c_float()
+        torch.cuda.synchronize(dev)
+        _lib.check(self.L.mtaz_net_time(self.h, c_void_p(pos.data_ptr()), n, 1, 1, ctypes.byref(ms),
+                                        st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        rec = st[nwg * 6:].reshape(-1)[:n]
+        return (rec >> np.uint64(32)).astype(np.int64), (rec & np.uint64(0xffffffff)).astype(np.int64)
+
     # ---- batched self-play -----------------------------------------------------------------------
     def set_precision(self, precision):
         """'f16x3' (default, k_net_y: fp16 hi/lo split, three f16 MFMA passes, fp32-accurate to ~1e-7;

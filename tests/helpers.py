@@ -128,7 +128,10 @@ def stress_network(name='stress'):
     updates in the C5 loop at lr 0.02, trunk activations in the thousands, legal-logit spreads up
     to ~80 on its fixture positions, its value head collapsed to a constant.  'stress4' (round 4,
     pinned by make_golden_r4.py): 20 updates at lr 0.003 with half the games from endgame starts,
-    a value head whose outputs vary (-0.26 .. 0.33 on its fixture positions)."""
+    a value head whose outputs vary (-0.26 .. 0.33 on its fixture positions).  'stress5' (round 5,
+    tools/make_stress5.py, pinned by make_golden_r5.py): stress4 with its residual trunk in 2^7
+    larger units, an exact reparametrisation (the reference's outputs are stress4's bit for bit)
+    that puts k_net_y's per-board exponents at 1-4 on every fixture position."""
     import json
     import os
     from safetensors.torch import load_file

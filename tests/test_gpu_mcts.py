@@ -78,21 +78,19 @@ def test_trees_bit_exact_vs_oracle(memo, spill):
 
 def _net(kind):
     """seed0: torch.manual_seed(0); Network().  stress: the round-3 stress checkpoint (trunk
-    activations in the thousands; its k_net_y stored-units exponents leave 0)."""
+    activations in the thousands; its k_net_y stored-units exponents leave 0 on a few positions).
+    stress5: stress4 with its trunk in 2^7 larger units (exponents 1-4 on every position and 18 of
+    the 19 trunk layers, a value head whose outputs vary; tests/golden/make_golden_r5.py)."""
     import torch
     from minitchess_alphazero_amd.network import Network
+    from helpers import stress_network
     if kind == 'seed0':
         torch.manual_seed(0)
         return Network()
-    from safetensors.torch import load_file
-    from conftest import GOLDEN
-    import os
-    net = Network()
-    net.load_state_dict(load_file(os.path.join(GOLDEN, 'stress', 'stress.safetensors')))
-    return net.eval()
+    return stress_network(kind)
 
 
-@pytest.mark.parametrize('kind', ['seed0', 'stress'])
+@pytest.mark.parametrize('kind', ['seed0', 'stress', 'stress5'])
 def test_leaf_memo_leaves_games_unchanged(kind):
     """The leaf memo changes which leaves the network evaluates, not the games: with the GPU network,
     the per-game memo, the per-game + batch memo and no memo give identical records, and computed +
@@ -206,7 +204,7 @@ def test_cpp_driver_equals_python_driver():
         assert [r['reward'] for r in a] == [r['reward'] for r in b]
 
 
-@pytest.mark.parametrize('kind', ['seed0', 'stress'])
+@pytest.mark.parametrize('kind', ['seed0', 'stress', 'stress5'])
 def test_games_independent_of_batch_composition(kind):
     """Per-game results depend only on the game's seed (the multi-GPU sharding contract), also on a
     trained net whose stored-units exponents leave 0: 40 games in one engine (up to

@@ -208,7 +208,8 @@ def test_y_tap_skip_bit_identical():
 
 
 @pytest.mark.parametrize('precision,net_kind', [('f16f8', 'seed0'), ('f16f8', 'tiny'), ('f16x3', 'seed0'),
-                                               ('f16x3', 'tiny'), ('f16x3', 'wide'), ('f16x3', 'stress')])
+                                               ('f16x3', 'tiny'), ('f16x3', 'wide'), ('f16x3', 'stress'),
+                                               ('f16x3', 'stress5')])
 def test_tail_launches_bit_identical(net_kind, precision):
     """The tail-balanced board assignment (k_net_z, k_net_y: the boards beyond the full rounds of
     4 x CUs go to workgroups of 1, 2 or 3 boards) computes every board exactly as 4 boards per
@@ -226,7 +227,7 @@ def test_tail_launches_bit_identical(net_kind, precision):
     import torch
     torch.manual_seed(0)
     net = {'seed0': Network, 'wide': _wide_range_net, 'tiny': _tiny_activation_net,
-           'stress': _stress_net}[net_kind]()
+           'stress': _stress_net, 'stress5': lambda: _stress_net('stress5')}[net_kind]()
     fens = random_fens(400, seed=29)
     eng = Engine(n_games=4096, sims=4)
     eng.set_precision(precision)
@@ -338,17 +339,18 @@ def test_dynamic_range_beyond_f16(precision, var):
                 assert legal[int(np.argmax(logits[i][legal]))] == legal[int(np.argmax(p[i][legal]))]
 
 
-def _stress_net():
+def _stress_net(name='stress'):
     """The round-3 stress checkpoint (tests/golden/stress/): trained in the C5 loop, trunk
-    activations in the thousands."""
+    activations in the thousands.  'stress5': stress4 with its trunk in 2^7 larger units (k_net_y's
+    exponents 1-4 on every board, values that vary; tests/golden/make_golden_r5.py)."""
     from safetensors.torch import load_file
     from minitchess_alphazero_amd.network import Network
     net = Network()
-    net.load_state_dict(load_file(os.path.join(GOLDEN, 'stress', 'stress.safetensors')))
+    net.load_state_dict(load_file(os.path.join(GOLDEN, name, f'{name}.safetensors')))
     return net.eval()
 
 
-@pytest.mark.parametrize('net_kind', ['wide', 'stress'])
+@pytest.mark.parametrize('net_kind', ['wide', 'stress', 'stress5'])
 def test_board_results_independent_of_batch(net_kind):
     """a board's logits and value do not depend on the other boards of its batch or
     workgroup (the reference evaluates every leaf batch-1, exp/agent.py:67-69), also once the
@@ -358,7 +360,7 @@ def test_board_results_independent_of_batch(net_kind):
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from tests_positions import random_fens
-    net = {'wide': _wide_range_net, 'stress': _stress_net}[net_kind]()
+    net = {'wide': _wide_range_net, 'stress': _stress_net, 'stress5': lambda: _stress_net('stress5')}[net_kind]()
     fens = random_fens(1300, seed=41)
     pos = np.stack([pos_from_fen(f) for f in fens])
     eng = Engine(n_games=4096, sims=4)

@@ -40,7 +40,7 @@ TOL = 1e-5
 EXACT = ['f16x3', 'fp32']          # the precisions whose north_star claim covers this net
 
 
-CKPTS = ['stress', 'stress4']
+CKPTS = ['stress', 'stress4', 'stress5']
 
 
 def _fixture(name='stress'):
@@ -88,6 +88,55 @@ def test_stress4_checkpoint_pinned_and_values_vary():
     assert meta['training']['summary']['criteria']['min_iteration'] >= 19     # >= 20 learner updates
     assert ref_v.max() - ref_v.min() >= 0.4 and ref_v.std() >= 0.05
     assert meta['game_end']['moves'][-1]['reward'] != 0                       # a decisive reference game
+
+
+def test_stress5_checkpoint_pinned_exponents_and_values():
+    """stress5 (tools/make_stress5.py: stress4's trunk in 2^7 larger units) drives
+    k_net_y's per-board stored-units exponent off 0 -- on every fixture position, on 18 of the 19
+    trunk layers (the emulation tools/net_range.py recorded by make_golden_r5.py) -- with a value
+    head whose reference outputs vary; the reference's outputs equal its outputs on stress4 bit for
+    bit (an exact reparametrisation)."""
+    meta = load_golden('stress5')
+    stress_network('stress5')
+    _, _, ref_v = _fixture('stress5')
+    ex = meta['k_net_y_exponents']
+    assert ex['boards_any_xs_pos'] == ex['boards'] == meta['positions'] and ex['layers_xs_pos'] >= 18
+    assert ex['xs_max'] >= 3
+    assert ref_v.std() >= 0.05 and ref_v.max() - ref_v.min() >= 0.4
+    assert meta['logits_finite']
+    assert meta['derivation']['reference_outputs_equal_stress4'] == meta['positions']
+    # the reference learner's own regime was tried first (profiles/r05/train_lr): the value head died
+    runs = meta['derivation']['training_runs']
+    assert any(r['lr'] == 0.2 for r in runs) and all(r['value_dead_from_update'] is not None for r in runs)
+
+
+def test_stress5_kernel_exponents_equal_the_emulation():
+    """The exponents k_net_y itself picks on stress5 (the stamp-instrumented build's per-board
+    records, Engine.net_exponents) equal tools/net_range.py's recomputation of the kernel's bound
+    from a float64 forward, board by board and layer by layer: the fixtures below really run the
+    nonzero-exponent path (and stress4's run none of it)."""
+    import sys
+    from minitchess_alphazero_amd.engine import Engine
+    from minitchess_alphazero_amd.environment import pos_from_fen
+    from conftest import REPO
+    sys.path.insert(0, os.path.join(REPO, 'tools'))
+    from net_range import fens_profile
+    for name in ('stress5', 'stress4'):
+        fens = _fixture(name)[0]
+        eng = Engine(n_games=64, sims=4)
+        eng.set_precision('f16x3')
+        net = stress_network(name)
+        eng.set_weights(net)
+        xmax, mask = eng.net_exponents(np.stack([pos_from_fen(f) for f in fens]))
+        xs = fens_profile(net.state_dict(), fens)['xs']                       # [19 layers, boards]
+        emu_mask = ((xs > 0).astype(np.int64) << np.arange(xs.shape[0])[:, None]).sum(axis=0)
+        assert np.array_equal(xmax, xs.max(axis=0)), name
+        assert np.array_equal(mask, emu_mask), name
+        if name == 'stress5':
+            assert (xmax > 0).all()
+        else:
+            assert (mask == 0).all()
+        eng.close()
 
 
 @pytest.mark.parametrize('name', CKPTS)
@@ -171,18 +220,19 @@ def test_stress_gpu_net_64_sims_vs_reference(precision):
     _l3('stress_64', precision, stress_network(), ref.eval(), [load_golden('stress')['stress_64']])
 
 
+@pytest.mark.parametrize('name', ['stress4', 'stress5'])
 @pytest.mark.parametrize('game', ['game_start', 'game_end'])
-def test_stress4_host_leaves_64_sims_equal_reference(game):
-    """L1 on stress4: the reference's 64-sim games (from STARTING_FEN, and the decisive one from an
-    endgame start), leaves evaluated batch-1 on the host exactly as exp/agent.py:66-69; every pi,
-    action and reward bit-exact."""
+def test_stress4_host_leaves_64_sims_equal_reference(game, name):
+    """L1 on stress4 and stress5: the reference's 64-sim games (from STARTING_FEN, and one from an
+    endgame start: decisive for stress4), leaves evaluated batch-1 on the host exactly as
+    exp/agent.py:66-69; every pi, action and reward bit-exact."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import STARTING_FEN
     from oracle.mcts import TorchNetEvaluator
     from oracle.net import Network as RefNet
-    gm = load_golden('stress4')[game]
+    gm = load_golden(name)[game]
     ref = RefNet()
-    ref.load_state_dict(stress_network('stress4').state_dict())
+    ref.load_state_dict(stress_network(name).state_dict())
     eng = Engine(n_games=1, sims=gm['sims'])
     recs, _ = drive_engine(eng, 1, gm['sims'], [gm['seed']], evaluator=TorchNetEvaluator(ref.eval()),
                            start_fen=gm['start'] or STARTING_FEN)
@@ -190,10 +240,12 @@ def test_stress4_host_leaves_64_sims_equal_reference(game):
     assert [x['reward'] for x in recs[0]] == [x['reward'] for x in gm['moves']]
 
 
-def test_stress4_gpu_net_64_sims_vs_reference():
-    """L3 on stress4 with the default network (k_net_y), the game from STARTING_FEN."""
+@pytest.mark.parametrize('name', ['stress4', 'stress5'])
+def test_stress4_gpu_net_64_sims_vs_reference(name):
+    """L3 on stress4 and stress5 with the default network (k_net_y), the game from STARTING_FEN
+    (on stress5 with the exponents off 0 on every layer but the stem)."""
     from test_gpu_search_parity import _l3
     from oracle.net import Network as RefNet
     ref = RefNet()
-    ref.load_state_dict(stress_network('stress4').state_dict())
-    _l3('stress4_start', 'f16x3', stress_network('stress4'), ref.eval(), [load_golden('stress4')['game_start']])
+    ref.load_state_dict(stress_network(name).state_dict())
+    _l3(f'{name}_start', 'f16x3', stress_network(name), ref.eval(), [load_golden(name)['game_start']])

@@ -130,12 +130,12 @@ def test_terminal_revisit_quirk(golden):
         assert seen_quirk
 
 
-@pytest.mark.parametrize('name', ['stress', 'stress4'])
+@pytest.mark.parametrize('name', ['stress', 'stress4', 'stress5'])
 def test_trained_checkpoint_outputs(name):
     """The oracle's network (exp/policy.py restated) on the trained checkpoints reproduces the
     reference's own outputs (make_golden_r3.py / make_golden_r4.py) on fixture positions: the
     oracle the GPU parity tests compare against is pinned on these nets too, varying values
-    (stress4) included."""
+    (stress4, stress5) and k_net_y's nonzero exponent range (stress5) included."""
     import os
     import torch
     from safetensors.torch import load_file
@@ -151,3 +151,25 @@ def test_trained_checkpoint_outputs(name):
             p, v = n(encoder.process_observation(str(z['fens'][i])))
             assert np.max(np.abs(p[0].numpy() - z['logits'][i])) <= 1e-5 * max(1.0, float(np.abs(z['logits'][i]).max()))
             assert abs(float(v.item()) - float(z['values'][i])) <= 1e-6
+
+
+def test_stress5_is_an_exact_reparametrisation_of_stress4():
+    """tools/make_stress5.py: the committed stress5 is stress4 with its trunk in 2^7 larger units
+    (recomputed here from stress4 and compared tensor by tensor); the emulated k_net_y exponents
+    (tools/net_range.py) are 0 everywhere on stress4 and 1..4 on every stress5 fixture position."""
+    import os
+    import sys
+    import torch
+    from safetensors.torch import load_file
+    from conftest import GOLDEN, REPO, load_golden
+    sys.path.insert(0, os.path.join(REPO, 'tools'))
+    from make_stress5 import rescale
+    from net_range import fens_profile
+    s4 = load_file(os.path.join(GOLDEN, 'stress4', 'stress4.safetensors'))
+    s5 = load_file(os.path.join(GOLDEN, 'stress5', 'stress5.safetensors'))
+    again = rescale(s4, load_golden('stress5')['derivation']['scale_log2'])
+    assert set(again) == set(s5) and all(torch.equal(again[k], s5[k]) for k in s5)
+    fens = [str(f) for f in np.load(os.path.join(GOLDEN, 'stress5_net.npz'))['fens'][::8]]
+    assert (fens_profile(s4, fens)['xs'] == 0).all()
+    xs5 = fens_profile(s5, fens)['xs']
+    assert (xs5.max(axis=0) >= 1).all() and xs5.max() <= 4

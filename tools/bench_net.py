@@ -60,10 +60,10 @@ def main():
             eng.set_precision(prec)
             _lib.check(eng.L.mtaz_set_net_variant(eng.h, int(var)))
             ms = ctypes.c_float()
-            st = np.zeros(nwg * 6, np.uint64)
+            st = np.zeros(nwg * 10, np.uint64)   # phase stamps [nwg][6], then exponent records [nwg][4]
             _lib.check(eng.L.mtaz_net_time(eng.h, ctypes.c_void_p(d.data_ptr()), args.n, args.iters, 1,
                                            ctypes.byref(ms), st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
-            st = st.reshape(nwg, 6).astype(np.float64)
+            st = st[:nwg * 6].reshape(nwg, 6).astype(np.float64)
             res[v]['ms'].append(ms.value)
             res[v]['cycles'].append(float(st[:, 4].mean()))
             res[v]['ghz'].append(float((st[:, 4] / (st[:, 5] * 10.0)).mean()))   # cycles / (ticks * 10 ns) -> GHz

@@ -58,9 +58,14 @@ def main():
     for k, v in sorted(tails.items()):
         act = [x for x in v if x > 30]
         emp = sorted(x for x in v if x <= 30)
+        hist = collections.Counter(int(x // 50) * 50 for x in act)
         out['tail_instances'][k] = {'launches': len(v), 'active': len(act),
                                     'active_mean_us': sum(act) / len(act) if act else None,
-                                    'empty_median_us': emp[len(emp) // 2] if emp else None}
+                                    'active_sum_us': sum(act),
+                                    'empty_median_us': emp[len(emp) // 2] if emp else None,
+                                    # active launches by duration (50-us bins: the 1-, 2- and 3-board
+                                    # instances fall in separate clusters)
+                                    'active_hist_50us': {str(b): hist[b] for b in sorted(hist)}}
     for k, v in gaps.items():
         if len(v) >= 100:
             out['gap_median_us'][k] = sorted(v)[len(v) // 2]
