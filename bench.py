@@ -281,6 +281,10 @@ def main():
                          'event (Engine.set_sync_mode); -1 (default) = 1 when this rank has a share of a '
                          'multi-rank node (N > 1 or --rank-share), else 0 (profiles/r05/hostshare: +2.1%% '
                          'at the 2-CPU share, neutral at 16)')
+    ap.add_argument('--defer', type=int, default=1, choices=[0, 1],
+                    help='deferred tails (Engine.set_defer): 1 (default) = each simulation wave evaluates whole '
+                         'rounds of 4 boards x CUs and the rest of its leaves wait for the next wave; 0 = every '
+                         'leaf every wave (round 4). Results are identical')
     ap.add_argument('--one-thread-during-warmup', type=int, default=1, choices=[0, 1],
                     help='1 (default): run the CPU baseline 1-thread legs during engine setup and the '
                          'untimed warm-up steps (collected before the timed region); 0: after the timed '
@@ -374,6 +378,7 @@ def main():
     eng.set_pipeline(args.groups)
     sync_mode = args.sync_mode if args.sync_mode >= 0 else int(world > 1 or rank_share is not None)
     eng.set_sync_mode(sync_mode)
+    eng.set_defer(args.defer)
     eng.evaluate(np.stack([start_position()] * 8))    # load code objects before timing
     LEG_HOST_THREADS = 2
     if legs is not None:
@@ -429,7 +434,7 @@ def main():
             dist.barrier()
 
     KEYS = ('sims', 'nn_evals', 'memo_hits', 'memo_batch_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
-            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms', 'choice_ms', 'gap_ms')
+            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms', 'choice_ms', 'gap_ms', 'extra_waves', 'moves')
 
     import resource
 
@@ -468,7 +473,10 @@ def main():
                 'memo_batch_hit_frac': tot['memo_batch_hits'] / ref_evals if ref_evals else 0.0,
                 'nn_evals_per_s': tot['nn_evals'] / dt, 'nn_evals_reference_per_s': ref_evals / dt,
                 'terminal_sims_per_game': tot['terminal_sims'] / games, 'decisive_games': int(tot['decisive']),
-                'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12}
+                'nn_tflops_algorithmic': tot['nn_evals'] * FLOP_PER_EVAL / dt / 1e12,
+                # simulation waves (one network launch each) and, with deferred tails, the waves that
+                # ended moves for the games whose leaves had waited
+                'waves': int(tot['waves']), 'extra_waves': int(tot['extra_waves'])}
 
     dt, tot, prec = timed(eng, args.steps, 'main')
     games = G * args.steps * world
@@ -497,6 +505,7 @@ def main():
         eng36.set_memo(args.memo)
         eng36.set_host_threads(eng_threads)
         eng36.set_sync_mode(sync_mode)
+        eng36.set_defer(args.defer)
         eng36.evaluate(np.stack([start_position()] * 8))
         dt3, tot3, prec3 = timed(eng36, 1, f'{args.default_sims} sims')
         at_default = {'sims_per_move': args.default_sims, 'value': G * world / dt3, 'unit': 'games/s', 'steps': 1,
@@ -593,6 +602,7 @@ def main():
         'host_cpu_s': tot['host_cpu_ms'] / 1e3 / world,
         'host_cpus_busy': tot['host_cpu_ms'] / 1e3 / world / dt,
         'sync_mode': sync_mode,
+        'defer': args.defer,
         'mtaz_src_sha256': lib_hash,
     }
     if rank_share is not None:

@@ -79,6 +79,10 @@ struct Games {
   uint32_t* path_node;    // [G*DMAX] chain of (node, edge) of the current sim
   uint32_t* path_edge;
   int32_t* path_len;
+  // deferred-tail play (mtaz_set_defer): simulations this move has started per game (the noise
+  // draw index of the next one); a game whose leaf was deferred keeps it in Leaves::gnode and
+  // selects again only after that leaf's backup
+  int32_t* simc;
   Pos* hist;              // [G*HMAX] game positions before each move (repetition)
   int32_t* nhist;
   int DMAX, HMAX;
@@ -238,7 +242,15 @@ void launch_reset_trees(const Dev& d, const int32_t* trees, int ntrees, bool all
 void launch_move_begin(const Dev& d, hipStream_t s);
 // k_select + k_leaf_compact; count_log (optional, device) receives [leaf count, memo hits], ev_mid
 // (optional) is recorded between the two kernels
-void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log = nullptr, hipEvent_t ev_mid = nullptr);
+// defer (mtaz_set_defer): 0 = every game selects simulation `sim` and every leaf is evaluated this
+// wave; 1 = games select their own next simulation (Games::simc) unless a deferred leaf is
+// pending, the leaf list is ordered by lag (largest first), and when `cut` is set only the whole
+// rounds of `round` leaves are evaluated (the rest stay pending for the next wave)
+void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log = nullptr, hipEvent_t ev_mid = nullptr,
+                   int defer = 0, int cut = 0, int round = 0);
+// after a deferred-tail move's regular waves: the waves still needed (max over games of the
+// simulations not yet started + a pending leaf) into *out
+void launch_remaining(const Dev& d, int32_t* out, hipStream_t s);
 #ifdef MTAZ_NET_DIAG
 int diag_select_stamps(unsigned long long* out8, int reset);   // k_select phase cycles (diag library)
 #endif

@@ -318,6 +318,10 @@ __global__ __launch_bounds__(64) void k_move_begin(Dev D) {
   __shared__ LegalLds s_l;
   __shared__ RuleTables s_rt;
   const int g = blockIdx.x, lane = threadIdx.x;
+  if (lane == 0) {   // a move starts with no simulation begun and no leaf pending
+    D.gm.simc[g] = 0;
+    D.lf.gnode[g] = NONE;
+  }
   if (!D.gm.active[g]) {
     if (lane == 0) { D.gm.root_k[g] = 0; D.gm.root_new[g] = 0; }
     return;
@@ -384,16 +388,28 @@ __device__ unsigned long long g_sel_cyc[SEL_STAMP_GAMES * 8];
 #define SEL_FIN()
 #endif
 
-__global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
+__global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
 #pragma clang fp contract(off)
   __shared__ LegalLds s_l;
   __shared__ RuleTables s_rt;
   const int g = blockIdx.x, lane = threadIdx.x;
-  if (lane == 0) {
-    D.lf.gnode[g] = NONE;
-    D.lf.ghit[g] = 0;
+  if (!defer) {
+    if (lane == 0) {
+      D.lf.gnode[g] = NONE;
+      D.lf.ghit[g] = 0;
+    }
+    if (!D.gm.active[g]) return;
+  } else {
+    // deferred-tail play: the game's own next simulation, unless its last leaf is still pending
+    // (deferred by k_leaf_compact) or it has started all of them.  A game's simulations run in
+    // order, one at a time, exactly as in lockstep; only the wave each one runs in moves.
+    if (lane == 0) D.lf.ghit[g] = 0;
+    if (!D.gm.active[g] || D.lf.gnode[g] != NONE) return;
+    const int s = D.gm.simc[g];
+    if (s >= D.pr.sims) return;
+    if (lane == 0) D.gm.simc[g] = s + 1;
+    sim = s;
   }
-  if (!D.gm.active[g]) return;
 #ifdef MTAZ_NET_DIAG
   unsigned long long sel_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long sel_t0 = __builtin_amdgcn_s_memtime();
@@ -624,58 +640,116 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim) {
   }
 }
 
-// The leaf batch in game order: one workgroup; per chunk of 4,096 games thread i holds games
-// 4i..4i+3 in registers (their leaf, agent and position in one round of loads: loads placed after
-// the stores would wait for them), a block scan of the per-thread counts places its leaves.
-// Also logs the count and the memo hits of the game and batch memos (count_log[0..2], when given).
-__global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restrict__ count_log) {
-  constexpr int PER = 4;
+// The leaf batch: one workgroup; per chunk of 4,096 games thread i holds games 4i..4i+3 in registers
+// (their leaf, agent and position in one round of loads: loads placed after the stores would wait
+// for them), a block scan of the per-thread counts places its leaves.  Classic play lists the
+// leaves in game order.  Deferred-tail play (defer) lists them by lag, largest first, game order
+// within a lag (lag = waves since the game selected the leaf's simulation: a pending leaf of an
+// earlier wave comes before the new ones), and with `cut` evaluates only the whole rounds of
+// `round` leaves (4 boards x the CUs: the network's full rounds), the rest staying pending.
+// Also logs the evaluated count and the memo hits of the game and batch memos (count_log[0..2]).
+__global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restrict__ count_log, int wave, int defer,
+                                                       int cut, int round) {
+  constexpr int PER = 4, NBK = 4;
   __shared__ int s_w[16];
   __shared__ int s_hits[2];
+  __shared__ int s_bk[NBK];   // leaves per lag bucket (pass 1), then the bucket's next slot
+  __shared__ int s_smax;
   const int G = D.pr.G, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid < 2) s_hits[tid] = 0;
+  if (tid < NBK) s_bk[tid] = 0;
+  if (tid == 0) s_smax = 0;
+  __syncthreads();
+  if (defer) {   // pass 0: the most advanced leaf's simulation index
+    int m = 0;
+    for (int g = tid; g < G; g += 1024)
+      if (D.lf.gnode[g] != NONE) m = max(m, D.gm.simc[g] - 1);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if (lane == 0) atomicMax(&s_smax, m);
+    __syncthreads();
+  }
+  // lag bucket of game g's leaf, 0 = the largest lag behind the most advanced leaf (listed first)
+  const int smax = s_smax;
+  auto bucket = [&](int g) {
+    if (!defer) return 0;
+    const int lag = smax - (D.gm.simc[g] - 1);
+    return NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
+  };
+  if (defer) {   // pass 1: leaves per bucket
+    int cb[NBK] = {0, 0, 0, 0};
+    for (int g = tid; g < G; g += 1024)
+      if (D.lf.gnode[g] != NONE) {
+        const int b = bucket(g);
+#pragma unroll
+        for (int q = 0; q < NBK; ++q) cb[q] += b == q;
+      }
+#pragma unroll
+    for (int q = 0; q < NBK; ++q) {
+      int x = cb[q];
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+      if (lane == 0 && x) atomicAdd(&s_bk[q], x);
+    }
+    __syncthreads();
+    if (tid == 0) {   // exclusive prefix: each bucket's first slot
+      int acc = 0;
+      for (int q = 0; q < NBK; ++q) {
+        const int x = s_bk[q];
+        s_bk[q] = acc;
+        acc += x;
+      }
+    }
+    __syncthreads();
+  }
   int base = 0, hits = 0, bhits = 0;
   for (int c0 = 0; c0 < G; c0 += 1024 * PER) {
     const int g0 = c0 + tid * PER;
     uint32_t nd[PER];
-    int ag[PER];
+    int ag[PER], bk[PER];
     Pos ps[PER];
-    int c = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const bool in = g0 + j < G;
       nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
       ag[j] = in ? D.gm.agent[g0 + j] : 0;
       ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
+      bk[j] = (in && nd[j] != NONE) ? bucket(g0 + j) : 0;
       const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
       hits += hk == 1;
       bhits += hk == 2;
     }
+    // one block scan per bucket (classic play: bucket 0 only)
+    for (int q = 0; q < (defer ? NBK : 1); ++q) {
+      int c = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) c += nd[j] != NONE;
-    const int incl = wave_incl_scan(c);
-    if (lane == 63) s_w[w] = incl;
-    __syncthreads();
-    int slot = base + incl - c, tot = 0;
+      for (int j = 0; j < PER; ++j) c += nd[j] != NONE && bk[j] == q;
+      const int incl = wave_incl_scan(c);
+      if (lane == 63) s_w[w] = incl;
+      __syncthreads();
+      int slot = (defer ? s_bk[q] : base) + incl - c, tot = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int x = s_w[i];
-      slot += i < w ? x : 0;
-      tot += x;
-    }
-    __syncthreads();   // s_w is rewritten by the next chunk
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      if (nd[j] != NONE) {
-        const int g = g0 + j;
-        D.lf.game[slot] = g;
-        D.lf.tree[slot] = 2 * g + ag[j];
-        D.lf.node[slot] = nd[j];
-        D.lf.pos[slot] = ps[j];
-        ++slot;
+      for (int i = 0; i < 16; ++i) {
+        const int x = s_w[i];
+        slot += i < w ? x : 0;
+        tot += x;
       }
+      __syncthreads();   // s_w is rewritten by the next scan, s_bk read
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if (nd[j] != NONE && bk[j] == q) {
+          const int g = g0 + j;
+          D.lf.game[slot] = g;
+          D.lf.tree[slot] = 2 * g + ag[j];
+          D.lf.node[slot] = nd[j];
+          D.lf.pos[slot] = ps[j];
+          ++slot;
+        }
+      }
+      if (defer) {
+        if (tid == 0) s_bk[q] += tot;
+        __syncthreads();
+      }
+      base += tot;
     }
-    base += tot;
   }
   for (int o = 32; o > 0; o >>= 1) {
     hits += __shfl_xor(hits, o, 64);
@@ -685,20 +759,48 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
   if (lane == 0 && bhits) atomicAdd(&s_hits[1], bhits);
   __syncthreads();
   if (tid == 0) {
-    *D.lf.count = base;
+    // the evaluated count: every leaf, or (cut) the whole rounds of them when there is one
+    const int n = (cut && round > 0 && base >= round) ? base - base % round : base;
+    *D.lf.count = n;
     if (count_log) {
-      count_log[0] = base;
+      count_log[0] = n;
       count_log[1] = s_hits[0];
       count_log[2] = s_hits[1];
     }
   }
 }
 
-// one simulation's selection: k_select, then the dense leaf list and count
-void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log, hipEvent_t ev_mid) {
-  hipLaunchKernelGGL(k_select, dim3(d.pr.G), dim3(64), 0, s, d, sim);
+// one simulation's selection: k_select, then the leaf list and the evaluated count
+void launch_select(const Dev& d, int sim, hipStream_t s, int32_t* count_log, hipEvent_t ev_mid, int defer, int cut,
+                   int round) {
+  hipLaunchKernelGGL(k_select, dim3(d.pr.G), dim3(64), 0, s, d, sim, defer);
   if (ev_mid) (void)hipEventRecord(ev_mid, s);
-  hipLaunchKernelGGL(k_leaf_compact, dim3(1), dim3(1024), 0, s, d, count_log);
+  hipLaunchKernelGGL(k_leaf_compact, dim3(1), dim3(1024), 0, s, d, count_log, sim, defer, cut, round);
+}
+
+// waves a deferred-tail move still needs: max over active games of (sims not started) + (a leaf pending)
+__global__ __launch_bounds__(256) void k_remaining(Dev D, int32_t* __restrict__ out) {
+  __shared__ int s_m;
+  if (threadIdx.x == 0) s_m = 0;
+  __syncthreads();
+  int m = 0;
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < D.pr.G; g += gridDim.x * 256)
+    if (D.gm.active[g]) {
+      const int r = (D.pr.sims - D.gm.simc[g]) + (D.lf.gnode[g] != NONE ? 1 : 0);
+      m = r > m ? r : m;
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int x = __shfl_xor(m, o, 64);
+    m = x > m ? x : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(&s_m, m);
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, s_m);
+}
+
+void launch_remaining(const Dev& d, int32_t* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, 4, s);
+  hipLaunchKernelGGL(k_remaining, dim3(16), dim3(256), 0, s, d, out);
 }
 
 #ifdef MTAZ_NET_DIAG
@@ -770,6 +872,7 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
   const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
   backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i], lane);
+  if (lane == 0) D.lf.gnode[g] = NONE;   // evaluated: no longer pending (deferred-tail play)
 }
 
 void launch_memo_clear(const Dev& d, hipStream_t s) {

@@ -468,7 +468,7 @@ struct GameRec {
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
-  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_CHOICE_MS, ST_GAP_MS, ST_COUNT
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_CHOICE_MS, ST_GAP_MS, ST_EXTRA_WAVES, ST_COUNT
 };
 
 // Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
@@ -665,6 +665,11 @@ struct mtaz_engine {
   // signals, leaving its CPU to the other ranks' host work)
   int sync_mode = 0;
   hipEvent_t sync_ev = nullptr;
+  // deferred tails (mtaz_set_defer): in mtaz_play each wave evaluates only the whole rounds of
+  // 4 boards x ncu leaves; the rest wait for the next wave (Games::simc, k_leaf_compact)
+  int defer = 1;
+  int ncu = 0;
+  int32_t* d_remaining = nullptr;
 
   ~mtaz_engine() {
     group_pool.reset();
@@ -784,6 +789,7 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&gm.path_node, (size_t)G * gm.DMAX));
   ECHK(h->dalloc(&gm.path_edge, (size_t)G * gm.DMAX));
   ECHK(h->dalloc(&gm.path_len, G));
+  ECHK(h->dalloc(&gm.simc, G));
   ECHK(h->dalloc(&gm.hist, (size_t)G * gm.HMAX));
   ECHK(h->dalloc(&gm.nhist, G));
   HIPCHK(hipMemset(gm.active, 0, G));
@@ -810,6 +816,10 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&h->d_trees, T));
   h->count_log_cap = h->sims * (2 * max_moves + 8);   // waves; three ints each (leaves, game / batch memo hits)
   ECHK(h->dalloc(&h->d_count_log, 3 * (size_t)h->count_log_cap));
+  ECHK(h->dalloc(&h->d_remaining, 1));
+  HIPCHK(hipMemset(lf.gnode, 0xff, (size_t)G * 4));   // no leaf pending
+  HIPCHK(hipMemset(gm.simc, 0, (size_t)G * 4));
+  if (hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) h->ncu = 0;
   // exact sqrt(N.sum()) table: N.sum() <= sims * searches per agent
   const int sqn = tr.NC + 2;
   std::vector<double> sq(sqn);
@@ -1452,6 +1462,13 @@ extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
   return 0;
 }
 
+extern "C" int mtaz_set_defer(mtaz_engine* h, int mode) {
+  if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "defer must be 0 (every leaf each wave) or 1 (deferred tails)");
+  h->defer = mode;
+  for (mtaz_engine* p : h->parts) p->defer = mode;
+  return 0;
+}
+
 extern "C" int mtaz_set_sync_mode(mtaz_engine* h, int mode) {
   if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "sync mode must be 0 (stream sync) or 1 (blocking event)");
   h->sync_mode = mode;
@@ -1576,7 +1593,7 @@ extern "C" int mtaz_set_noise(mtaz_engine* h, const double* noise, const int64_t
   return 0;
 }
 
-static int sim_gpu(mtaz_engine* h, int sim) {
+static int sim_gpu(mtaz_engine* h, int sim, int defer = 0, int cut = 0) {
   // timing: per wave four events on the engine stream: [select begin, leaf compaction begin,
   // network begin, network end]
   hipEvent_t em = nullptr, eb = nullptr, ee = nullptr;
@@ -1592,7 +1609,8 @@ static int sim_gpu(mtaz_engine* h, int sim) {
     eb = h->ev[4 * h->wave + 2];
     ee = h->ev[4 * h->wave + 3];
   }
-  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + 3 * (size_t)h->wave : nullptr, em);
+  launch_select(h->d, sim, h->stream, h->wave < h->count_log_cap ? h->d_count_log + 3 * (size_t)h->wave : nullptr, em,
+                defer, cut, 4 * h->ncu);
   launch_network(h, h->d.lf.pos, h->d.lf.count, h->G, NET_LEAVES, nullptr, nullptr, eb, ee);
   launch_backup(h->d, h->stream);
   HIPCHK(hipGetLastError());
@@ -1865,6 +1883,7 @@ static int play_groups(mtaz_engine* h) {
     p->timing = h->timing;
     p->host_threads = std::max(1, h->host_threads / ng);   // the groups share this engine's threads
     p->sync_mode = h->sync_mode;
+    p->defer = h->defer;
     p->memo = h->memo;
     ECHK(ensure_batch_memo(p));
     sync_memo(p);
@@ -2011,12 +2030,26 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     if (t_gap >= 0) gap_ms += now_ms() - t_gap;
     for (int s0 = 0; s0 < h->sims; s0 = chunk_end(s0)) {
       // simulation s uses draw s - root_new <= s: the chunk holding draw s is on the stream first
-      for (int s = s0; s < chunk_end(s0); ++s) ECHK(sim_gpu(h, s));
+      // (with deferred tails a game runs simulation s in wave s or later)
+      for (int s = s0; s < chunk_end(s0); ++s) ECHK(sim_gpu(h, s, h->defer, h->defer));
       if (chunk_end(s0) < h->sims) {
         tr = now_ms();
         ECHK(draw_chunk(chunk_end(s0)));
         rng_ms += now_ms() - tr;
       }
+    }
+    if (h->defer) {
+      // deferred tails: the waves the games still need (simulations not yet started, a leaf still
+      // pending), each evaluating every leaf, so that every game ends the move with `sims` simulations
+      ts = now_ms();
+      launch_remaining(h->d, h->d_remaining, h->stream);
+      int32_t rem = 0;
+      HIPCHK(hipMemcpyAsync(&rem, h->d_remaining, 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(stream_wait(h));
+      sync_ms += now_ms() - ts;
+      if (rem > h->sims + 1) return set_err(MTAZ_E_FAIL, "deferred tails: %d waves pending", rem);
+      for (int i = 0; i < rem; ++i) ECHK(sim_gpu(h, h->sims + i, 1, 0));
+      h->stats[ST_EXTRA_WAVES] += rem;
     }
     // root visit counts, rows of the longest active legal list (not KMAX: 8x fewer bytes to the host)
     int kmx = 1;

@@ -25,7 +25,7 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
               'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap',
-              'memo_batch_hits', 'choice_ms', 'gap_ms']
+              'memo_batch_hits', 'choice_ms', 'gap_ms', 'extra_waves']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
@@ -159,6 +159,15 @@ class Engine:
     def set_host_threads(self, n=0):
         """Host threads of the per-move work (0 = the process's affinity mask, at most 16)."""
         _lib.check(self.L.mtaz_set_host_threads(self.h, int(n)))
+
+    def set_defer(self, mode=1):
+        """Deferred tails in play() (1, the default): each simulation wave evaluates only the whole
+        rounds of 4 boards x CUs of its leaves; the rest stay pending for the next wave, whose
+        list puts them first (a game selects again only after its leaf's backup, so its
+        simulations run in order, exactly as in lockstep), and each move ends with the waves its
+        lagging games still need.  0 = every leaf every wave (the round-4 schedule).  Results are
+        identical in both modes."""
+        _lib.check(self.L.mtaz_set_defer(self.h, int(mode)))
 
     def set_sync_mode(self, mode=0):
         """How the host thread waits for the engine's stream: 0 = hipStreamSynchronize (default),

@@ -242,3 +242,32 @@ def test_pipelined_groups_equal_single_stream():
         for g in range(len(ref)):
             assert compare_records(eps[g], ref[g])[2] is None, (groups, g)
         assert st['games'] == 8 and st['sims'] == one.stats()['sims']
+
+
+@pytest.mark.parametrize('kind,memo', [('seed0', 2), ('seed0', 0), ('stress5', 2)])
+def test_deferred_tails_leave_games_unchanged(kind, memo):
+    """Deferred tails (mtaz_set_defer, the play() default): a wave evaluates only whole rounds of
+    4 boards x CUs of its leaves and the rest wait, their games selecting again only after that
+    leaf's backup; each move ends with the waves the lagging games need.  Every game still runs its
+    simulations in order on the same tables, noise and network results, so the records equal the
+    every-leaf-every-wave schedule's bit for bit, and every expansion is evaluated or supplied by
+    the memo in both (the reference's count).  4096 games: the waves hold more than one round of
+    leaves, so leaves are really deferred (extra_waves > 0)."""
+    net = _net(kind)
+    out = {}
+    for defer in (0, 1):
+        eng = _engine(4096, 8, seed_base=900)
+        eng.set_weights(net)
+        eng.set_memo(memo)
+        eng.set_defer(defer)
+        st = eng.play()
+        out[defer] = (st, eng.records())
+        eng.close()
+    (s0, r0), (s1, r1) = out[0], out[1]
+    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+        assert np.array_equal(r1[key], r0[key]), key
+    assert s1['nn_evals'] + s1['memo_hits'] == s0['nn_evals'] + s0['memo_hits']
+    assert s1['sims'] == s0['sims'] and s1['terminal_sims'] == s0['terminal_sims']
+    assert s0['extra_waves'] == 0 and s1['extra_waves'] > 0
+    print(f"{kind} memo {memo}: {s1['extra_waves']:.0f} extra waves over {s1['moves']:.0f} moves; "
+          f"waves {s0['waves']:.0f} -> {s1['waves']:.0f}")
