@@ -759,8 +759,12 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
   if (lane == 0 && bhits) atomicAdd(&s_hits[1], bhits);
   __syncthreads();
   if (tid == 0) {
-    // the evaluated count: every leaf, or (cut) the whole rounds of them when there is one
-    const int n = (cut && round > 0 && base >= round) ? base - base % round : base;
+    // the evaluated count: every leaf, or (cut) the whole rounds of them when there is one and the
+    // rest would have gone to a tail launch (at most 3 boards per CU); a remainder above that runs
+    // as a partial round of 4-board workgroups in the main launch, which costs about what a full
+    // round does for nearly a round of boards, and is evaluated now
+    const int rem = round > 0 ? base % round : 0;
+    const int n = (cut && round > 0 && base >= round && rem <= 3 * (round / 4)) ? base - rem : base;
     *D.lf.count = n;
     if (count_log) {
       count_log[0] = n;

@@ -814,7 +814,9 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&h->d_leaf_codes, (size_t)G * KMAX));
   ECHK(h->dalloc(&h->d_leaf_k, G));
   ECHK(h->dalloc(&h->d_trees, T));
-  h->count_log_cap = h->sims * (2 * max_moves + 8);   // waves; three ints each (leaves, game / batch memo hits)
+  // waves (two per simulation and move: deferred tails add waves at the end of a move); three ints
+  // each (evaluated leaves, game / batch memo hits)
+  h->count_log_cap = 2 * h->sims * (2 * max_moves + 8);
   ECHK(h->dalloc(&h->d_count_log, 3 * (size_t)h->count_log_cap));
   ECHK(h->dalloc(&h->d_remaining, 1));
   HIPCHK(hipMemset(lf.gnode, 0xff, (size_t)G * 4));   // no leaf pending
@@ -2041,15 +2043,20 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     if (h->defer) {
       // deferred tails: the waves the games still need (simulations not yet started, a leaf still
       // pending), each evaluating every leaf, so that every game ends the move with `sims` simulations
-      ts = now_ms();
-      launch_remaining(h->d, h->d_remaining, h->stream);
-      int32_t rem = 0;
-      HIPCHK(hipMemcpyAsync(&rem, h->d_remaining, 4, hipMemcpyDeviceToHost, h->stream));
-      HIPCHK(stream_wait(h));
-      sync_ms += now_ms() - ts;
-      if (rem > h->sims + 1) return set_err(MTAZ_E_FAIL, "deferred tails: %d waves pending", rem);
-      for (int i = 0; i < rem; ++i) ECHK(sim_gpu(h, h->sims + i, 1, 0));
-      h->stats[ST_EXTRA_WAVES] += rem;
+      // (deferring too, so that they also run whole rounds; a game with a leaf pending or a
+      // simulation left needs at least one more wave, so every round of this loop makes progress)
+      for (int extra = 0;;) {
+        ts = now_ms();
+        launch_remaining(h->d, h->d_remaining, h->stream);
+        int32_t rem = 0;
+        HIPCHK(hipMemcpyAsync(&rem, h->d_remaining, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(stream_wait(h));
+        sync_ms += now_ms() - ts;
+        if (rem == 0) break;
+        if (extra + rem > 4 * h->sims + 8) return set_err(MTAZ_E_FAIL, "deferred tails: %d waves pending after %d", rem, extra);
+        for (int i = 0; i < rem; ++i, ++extra) ECHK(sim_gpu(h, h->sims + extra, 1, 1));
+        h->stats[ST_EXTRA_WAVES] += rem;
+      }
     }
     // root visit counts, rows of the longest active legal list (not KMAX: 8x fewer bytes to the host)
     int kmx = 1;
