@@ -147,7 +147,7 @@ int mtaz_set_host_threads(mtaz_engine* h, int n);
  * so the waiting thread sleeps instead of holding a CPU (8 ranks share one node's host cores:
  * bench.py --sync-mode, --rank-share).  Results are identical in both modes. */
 int mtaz_set_sync_mode(mtaz_engine* h, int mode);
-/* Deferred tails in mtaz_play (1 = default, 0 = off).  The network runs in full rounds of 4 boards
+/* Deferred tails in mtaz_play (1 = default, 0 = off, 2 = every remainder waits, partial rounds too).  The network runs in full rounds of 4 boards
  * per CU; a simulation wave whose leaf count n is not a multiple of that round (4 x CUs) used to
  * end with a tail launch whose 1-3-board workgroups stream all weights for few boards.  With
  * deferral a wave evaluates only the whole rounds; the remaining leaves stay pending and lead the
@@ -157,6 +157,9 @@ int mtaz_set_sync_mode(mtaz_engine* h, int mode);
  * draws and network results, so games, tables and records are identical in both modes; only the
  * wave each simulation runs in moves.  The fine-grained API (mtaz_sim_select ...) is unaffected. */
 int mtaz_set_defer(mtaz_engine* h, int mode);
+/* per-wave log of the last mtaz_play (up to max_waves): out[3 * w + 0] leaves evaluated,
+ * [+1] game-memo hits, [+2] batch-memo hits; returns the number of waves written */
+int mtaz_wave_log(mtaz_engine* h, int32_t* out, int max_waves);
 /* network-only timing harness: avg ms over `iters` launches on n device positions; with
  * stamped != 0 also, from one more launch of the stamp-instrumented build (4 boards per
  * workgroup, nwg = ceil(n / 4)), stamps_out[nwg * 10]: per workgroup [nwg][stem, conv K loops,

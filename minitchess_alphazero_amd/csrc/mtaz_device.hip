@@ -763,8 +763,9 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     // rest would have gone to a tail launch (at most 3 boards per CU); a remainder above that runs
     // as a partial round of 4-board workgroups in the main launch, which costs about what a full
     // round does for nearly a round of boards, and is evaluated now
+    // (cut 2: every remainder waits, the partial rounds too)
     const int rem = round > 0 ? base % round : 0;
-    const int n = (cut && round > 0 && base >= round && rem <= 3 * (round / 4)) ? base - rem : base;
+    const int n = (cut && round > 0 && base >= round && (cut == 2 || rem <= 3 * (round / 4))) ? base - rem : base;
     *D.lf.count = n;
     if (count_log) {
       count_log[0] = n;

@@ -1464,8 +1464,16 @@ extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
   return 0;
 }
 
+// per-wave log of the last mtaz_play: [waves][evaluated leaves, game-memo hits, batch-memo hits]
+extern "C" int mtaz_wave_log(mtaz_engine* h, int32_t* out, int max_waves) {
+  const int n = std::min(std::min(h->wave, h->count_log_cap), max_waves);
+  if (n > 0) HIPCHK(hipMemcpy(out, h->d_count_log, (size_t)n * 3 * 4, hipMemcpyDeviceToHost));
+  return n;
+}
+
 extern "C" int mtaz_set_defer(mtaz_engine* h, int mode) {
-  if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "defer must be 0 (every leaf each wave) or 1 (deferred tails)");
+  if (mode < 0 || mode > 2)
+    return set_err(MTAZ_E_FAIL, "defer must be 0 (every leaf each wave), 1 (deferred tails) or 2 (every remainder)");
   h->defer = mode;
   for (mtaz_engine* p : h->parts) p->defer = mode;
   return 0;
@@ -2033,7 +2041,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (int s0 = 0; s0 < h->sims; s0 = chunk_end(s0)) {
       // simulation s uses draw s - root_new <= s: the chunk holding draw s is on the stream first
       // (with deferred tails a game runs simulation s in wave s or later)
-      for (int s = s0; s < chunk_end(s0); ++s) ECHK(sim_gpu(h, s, h->defer, h->defer));
+      for (int s = s0; s < chunk_end(s0); ++s) ECHK(sim_gpu(h, s, h->defer ? 1 : 0, h->defer));
       if (chunk_end(s0) < h->sims) {
         tr = now_ms();
         ECHK(draw_chunk(chunk_end(s0)));
@@ -2054,7 +2062,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
         sync_ms += now_ms() - ts;
         if (rem == 0) break;
         if (extra + rem > 4 * h->sims + 8) return set_err(MTAZ_E_FAIL, "deferred tails: %d waves pending after %d", rem, extra);
-        for (int i = 0; i < rem; ++i, ++extra) ECHK(sim_gpu(h, h->sims + extra, 1, 1));
+        for (int i = 0; i < rem; ++i, ++extra) ECHK(sim_gpu(h, h->sims + extra, 1, h->defer));
         h->stats[ST_EXTRA_WAVES] += rem;
       }
     }

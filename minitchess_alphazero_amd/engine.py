@@ -165,9 +165,17 @@ class Engine:
         rounds of 4 boards x CUs of its leaves; the rest stay pending for the next wave, whose
         list puts them first (a game selects again only after its leaf's backup, so its
         simulations run in order, exactly as in lockstep), and each move ends with the waves its
-        lagging games still need.  0 = every leaf every wave (the round-4 schedule).  Results are
-        identical in both modes."""
+        lagging games still need.  0 = every leaf every wave (the round-4 schedule); 2 = every
+        remainder waits (also those the main launch would run as a partial round of 4-board
+        workgroups).  Results are identical in every mode."""
         _lib.check(self.L.mtaz_set_defer(self.h, int(mode)))
+
+    def wave_log(self, max_waves=1 << 17):
+        """Per-wave log of the last play(): int32 [waves, 3] = (leaves evaluated, game-memo hits,
+        batch-memo hits)."""
+        out = np.zeros((max_waves, 3), np.int32)
+        n = _lib.check(self.L.mtaz_wave_log(self.h, _p(out, c_int32), int(max_waves)))
+        return out[:n]
 
     def set_sync_mode(self, mode=0):
         """How the host thread waits for the engine's stream: 0 = hipStreamSynchronize (default),
