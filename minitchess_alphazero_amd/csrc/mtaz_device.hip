@@ -660,6 +660,92 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
   if (tid < NBK) s_bk[tid] = 0;
   if (tid == 0) s_smax = 0;
   __syncthreads();
+  if (defer && G <= 1024 * PER) {
+    // deferred-tail play, one chunk (G <= 4,096): every game's leaf, agent, position and lag loaded
+    // once into registers; block reductions give the most advanced leaf and the bucket sizes, then
+    // one block scan per bucket places the leaves
+    const int g0 = tid * PER;
+    uint32_t nd[PER];
+    int ag[PER], sc[PER], bk[PER];
+    Pos ps[PER];
+    int hits = 0, bhits = 0, m = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const bool in = g0 + j < G;
+      nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
+      ag[j] = in ? D.gm.agent[g0 + j] : 0;
+      ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
+      sc[j] = in ? D.gm.simc[g0 + j] - 1 : 0;
+      const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
+      hits += hk == 1;
+      bhits += hk == 2;
+      if (nd[j] != NONE) m = max(m, sc[j]);
+    }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if (lane == 0) atomicMax(&s_smax, m);
+    __syncthreads();
+    const int smx = s_smax;
+    int cb[NBK] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int lag = smx - sc[j];
+      bk[j] = NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
+#pragma unroll
+      for (int q = 0; q < NBK; ++q) cb[q] += nd[j] != NONE && bk[j] == q;
+    }
+#pragma unroll
+    for (int q = 0; q < NBK; ++q) {
+      int x = cb[q];
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+      if (lane == 0 && x) atomicAdd(&s_bk[q], x);
+    }
+    __syncthreads();
+    int first[NBK], total = 0;
+#pragma unroll
+    for (int q = 0; q < NBK; ++q) {
+      first[q] = total;
+      total += s_bk[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NBK; ++q) {
+      const int incl = wave_incl_scan(cb[q]);
+      if (lane == 63) s_w[w] = incl;
+      __syncthreads();
+      int slot = first[q] + incl - cb[q];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) slot += i < w ? s_w[i] : 0;
+      __syncthreads();   // s_w is rewritten by the next bucket's scan
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if (nd[j] != NONE && bk[j] == q) {
+          const int g = g0 + j;
+          D.lf.game[slot] = g;
+          D.lf.tree[slot] = 2 * g + ag[j];
+          D.lf.node[slot] = nd[j];
+          D.lf.pos[slot] = ps[j];
+          ++slot;
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      hits += __shfl_xor(hits, o, 64);
+      bhits += __shfl_xor(bhits, o, 64);
+    }
+    if (lane == 0 && hits) atomicAdd(&s_hits[0], hits);
+    if (lane == 0 && bhits) atomicAdd(&s_hits[1], bhits);
+    __syncthreads();
+    if (tid == 0) {
+      const int rem = round > 0 ? total % round : 0;
+      const int n = (cut && round > 0 && total >= round && (cut == 2 || rem <= 3 * (round / 4))) ? total - rem : total;
+      *D.lf.count = n;
+      if (count_log) {
+        count_log[0] = n;
+        count_log[1] = s_hits[0];
+        count_log[2] = s_hits[1];
+      }
+    }
+    return;
+  }
   if (defer) {   // pass 0: the most advanced leaf's simulation index
     int m = 0;
     for (int g = tid; g < G; g += 1024)

@@ -244,8 +244,8 @@ def test_pipelined_groups_equal_single_stream():
         assert st['games'] == 8 and st['sims'] == one.stats()['sims']
 
 
-@pytest.mark.parametrize('kind,memo', [('seed0', 2), ('seed0', 0), ('stress5', 2)])
-def test_deferred_tails_leave_games_unchanged(kind, memo):
+@pytest.mark.parametrize('kind,memo,mode', [('seed0', 2, 2), ('seed0', 0, 2), ('seed0', 2, 1), ('stress5', 2, 2)])
+def test_deferred_tails_leave_games_unchanged(kind, memo, mode):
     """Deferred tails (mtaz_set_defer, the play() default): a wave evaluates only whole rounds of
     4 boards x CUs of its leaves and the rest wait, their games selecting again only after that
     leaf's backup; each move ends with the waves the lagging games need.  Every game still runs its
@@ -255,7 +255,7 @@ def test_deferred_tails_leave_games_unchanged(kind, memo):
     leaves, so leaves are really deferred (extra_waves > 0)."""
     net = _net(kind)
     out = {}
-    for defer in (0, 1):
+    for defer in (0, mode):
         eng = _engine(4096, 8, seed_base=900)
         eng.set_weights(net)
         eng.set_memo(memo)
@@ -263,11 +263,11 @@ def test_deferred_tails_leave_games_unchanged(kind, memo):
         st = eng.play()
         out[defer] = (st, eng.records())
         eng.close()
-    (s0, r0), (s1, r1) = out[0], out[1]
+    (s0, r0), (s1, r1) = out[0], out[mode]
     for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
         assert np.array_equal(r1[key], r0[key]), key
     assert s1['nn_evals'] + s1['memo_hits'] == s0['nn_evals'] + s0['memo_hits']
     assert s1['sims'] == s0['sims'] and s1['terminal_sims'] == s0['terminal_sims']
     assert s0['extra_waves'] == 0 and s1['extra_waves'] > 0
-    print(f"{kind} memo {memo}: {s1['extra_waves']:.0f} extra waves over {s1['moves']:.0f} moves; "
+    print(f"{kind} memo {memo} defer {mode}: {s1['extra_waves']:.0f} extra waves over {s1['moves']:.0f} moves; "
           f"waves {s0['waves']:.0f} -> {s1['waves']:.0f}")
