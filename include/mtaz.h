@@ -147,8 +147,8 @@ int mtaz_set_host_threads(mtaz_engine* h, int n);
  * so the waiting thread sleeps instead of holding a CPU (8 ranks share one node's host cores:
  * bench.py --sync-mode, --rank-share).  Results are identical in both modes. */
 int mtaz_set_sync_mode(mtaz_engine* h, int mode);
-/* Deferred tails in mtaz_play (2 = default: every remainder waits, partial rounds too; 1 = only
- * remainders of at most 3 boards per CU, which would take a tail launch, wait; 0 = off).  The network runs in full rounds of 4 boards
+/* Deferred tails in mtaz_play (1 = default: remainders of at most 3 boards per CU, which would take
+ * a tail launch, wait; 2 = every remainder waits, partial rounds too; 0 = off).  The network runs in full rounds of 4 boards
  * per CU; a simulation wave whose leaf count n is not a multiple of that round (4 x CUs) used to
  * end with a tail launch whose 1-3-board workgroups stream all weights for few boards.  With
  * deferral a wave evaluates only the whole rounds; the remaining leaves stay pending and lead the

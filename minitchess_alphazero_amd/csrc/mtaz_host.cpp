@@ -666,9 +666,9 @@ struct mtaz_engine {
   int sync_mode = 0;
   hipEvent_t sync_ev = nullptr;
   // deferred tails (mtaz_set_defer): in mtaz_play each wave evaluates only the whole rounds of
-  // 4 boards x ncu leaves; the rest wait for the next wave (Games::simc, k_leaf_compact).  2 (the
-  // default): every remainder waits; 1: only those a tail launch would take
-  int defer = 2;
+  // 4 boards x ncu leaves; the rest wait for the next wave (Games::simc, k_leaf_compact).  1 (the
+  // default): the remainders a tail launch would take wait; 2: every remainder waits
+  int defer = 1;
   int ncu = 0;
   int32_t* d_remaining = nullptr;
 

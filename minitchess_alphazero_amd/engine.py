@@ -160,14 +160,16 @@ class Engine:
         """Host threads of the per-move work (0 = the process's affinity mask, at most 16)."""
         _lib.check(self.L.mtaz_set_host_threads(self.h, int(n)))
 
-    def set_defer(self, mode=2):
-        """Deferred tails in play() (2, the default): each simulation wave evaluates only the whole
-        rounds of 4 boards x CUs of its leaves; the rest stay pending for the next wave, whose
+    def set_defer(self, mode=1):
+        """Deferred tails in play() (1, the default): a simulation wave whose leaves beyond its whole
+        rounds of 4 boards x CUs would take a tail launch (at most 3 boards per CU) evaluates only
+        the whole rounds; the rest stay pending for the next wave, whose
         list puts them first (a game selects again only after its leaf's backup, so its
         simulations run in order, exactly as in lockstep), and each move ends with the waves its
-        lagging games still need.  0 = every leaf every wave (the round-4 schedule); 1 = only the
-        remainders a tail launch would take (at most 3 boards per CU) wait, a larger one runs as a
-        partial round of 4-board workgroups.  Results are identical in every mode."""
+        lagging games still need.  0 = every leaf every wave (the round-4 schedule); 2 = every
+        remainder waits, also one the main launch would run as a partial round of 4-board
+        workgroups (profiles/r05/t11: the same wall time with 32% more waves).  Results are
+        identical in every mode."""
         _lib.check(self.L.mtaz_set_defer(self.h, int(mode)))
 
     def wave_log(self, max_waves=1 << 17):
