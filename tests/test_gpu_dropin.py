@@ -7,6 +7,7 @@ import json
 import numpy as np
 import pytest
 
+from conftest import load_golden
 from helpers import compare_records
 
 pytestmark = pytest.mark.gpu
@@ -245,3 +246,35 @@ def test_puppet_global_stream_plays_the_reference_sequence():
     eng2.set_weights(net)
     eng2.play()
     assert compare_records(eps[1], eng2.episodes()[0])[2] is not None    # not a reseeded game
+
+
+def test_puppet_global_stream_equals_the_reference_fixture():
+    """VERDICT r4 missing #5, pinned to the reference: the drop-in SimulatePuppet with
+    rng_stream='global', after ONE np.random.seed(11), plays exactly the two consecutive episodes
+    the reference's own exp/* stack played that way (tests/golden/stream.json,
+    make_golden_r5_stream.py: app/base.py:108-124's sequence, referee turn carried over), every
+    observation, legal list, pi, action and reward, on the GPU engine (k_net_y leaves), and leaves
+    the global RandomState where the reference left it."""
+    import hashlib
+    import torch
+    from minitchess_alphazero_amd import puppet as pp
+    from minitchess_alphazero_amd.network import Network
+    fx = load_golden('stream')
+    pp.MINITCHESS_ALPHAZERO_VERSION = 'v-test'
+    torch.manual_seed(0)
+    net = Network()
+    p = pp.SimulatePuppet('u1', 'topic/eps', num_simulations=fx['sims'], rng_stream='global')
+    p.load_weights(net.state_dict(), 'w1')
+    p.remote_status = pp.MasterOfPuppetsStatus.SIMULATE
+    p.remote_version = 'v-test'
+    c = _Client()
+    np.random.seed(fx['seed'])
+    p.run_episodes(len(fx['episodes']), c)
+    st = np.random.get_state()
+    eps = [m[1]['episode'] for m in c.msgs]
+    assert len(eps) == len(fx['episodes'])
+    for got, ref in zip(eps, fx['episodes']):
+        assert compare_records(got, ref)[2] is None
+        assert [r['reward'] for r in got] == [r['reward'] for r in ref]
+    assert hashlib.sha256(st[1].tobytes()).hexdigest() == fx['rng_after']['key_sha256']
+    assert int(st[2]) == fx['rng_after']['pos']

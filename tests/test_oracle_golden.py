@@ -173,3 +173,34 @@ def test_stress5_is_an_exact_reparametrisation_of_stress4():
     assert (fens_profile(s4, fens)['xs'] == 0).all()
     xs5 = fens_profile(s5, fens)['xs']
     assert (xs5.max(axis=0) >= 1).all() and xs5.max() <= 4
+
+
+def test_oracle_global_stream_two_episodes():
+    """VERDICT r4 missing #5: the reference puppet's sequential stream (app/base.py:108-124: two
+    episodes through one referee after ONE np.random.seed, nothing reseeded, the referee's turn
+    carried over), recorded from the reference's own exp/* stack (make_golden_r5_stream.py), is
+    reproduced by the oracle draw for draw, the stream's final position included."""
+    import hashlib
+    from oracle import selfplay
+    from oracle.mcts import TorchNetEvaluator
+    from oracle.net import seed0_network
+    from conftest import load_golden
+    fx = load_golden('stream')
+    rng = np.random.RandomState(fx['seed'])
+    env = selfplay.MinitChessEnvironment()
+    ev = TorchNetEvaluator(seed0_network())
+    agents = [selfplay.SimpleAlphaZeroAgent(env, selfplay.SimpleAlphaZeroPolicy(ev), fx['sims'], rng=rng)
+              for _ in range(2)]
+    sink = []
+    cbs = [selfplay.InfoRecorder(sink), selfplay._MCInit(agents[0]), selfplay._MCInit(agents[1])]
+    selfplay.run_episodes(env, selfplay.RoundRobinReferee(agents), len(fx['episodes']), cbs)
+    assert len(sink) == len(fx['episodes'])
+    for got, ref in zip(sink, fx['episodes']):
+        assert [m['action'] for m in got] == [m['action'] for m in ref]
+        assert [m['observation'] for m in got] == [m['observation'] for m in ref]
+        assert [list(m['legal_moves']) for m in got] == [m['legal_moves'] for m in ref]
+        assert [list(m['pi']) for m in got] == [m['pi'] for m in ref]
+        assert [m['reward'] for m in got] == [m['reward'] for m in ref]
+    st = rng.get_state()
+    assert hashlib.sha256(st[1].tobytes()).hexdigest() == fx['rng_after']['key_sha256']
+    assert int(st[2]) == fx['rng_after']['pos']
