@@ -2018,10 +2018,13 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (int g = 0; g < G; ++g) js[g] = (int32_t)K;
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs.data(), G * 8, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), G * 4, hipMemcpyHostToDevice, h->stream));
-    // chunks [0, 1), [1, 9), [9, 17), ...: the GPU starts after one draw per game, and each later
-    // chunk is drawn while the previous chunk's simulations run
+    // chunks [0, 1), [1, 3), [3, 7), [7, 15), [15, 23), ...: the GPU starts after one draw per game,
+    // and each later chunk is drawn while the previous chunk's simulations run.  The chunks double
+    // up to 8 draws so that a chunk's draws never take longer than the simulations they overlap:
+    // a draw of every game costs about a fifth of a wave on 2 host threads (the 8-rank share), and
+    // round 4's [1, 9) after a single wave left the GPU idle for ~2 ms per move there
     constexpr int NCH = 8;
-    auto chunk_end = [&](int j0) { return std::min(j0 == 0 ? 1 : j0 + NCH, h->sims); };
+    auto chunk_end = [&](int j0) { return std::min(j0 + std::min(NCH, j0 + 1), h->sims); };
     auto draw_chunk = [&](int j0) {   // draws [j0, chunk_end(j0)) of every active game
       const int je = chunk_end(j0);
       parallel_for(G, h->host_threads, [&](int g) {
