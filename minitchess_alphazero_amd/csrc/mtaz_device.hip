@@ -22,14 +22,44 @@ int dev_upload_codec(const Codec& c) {
 
 // ---------------------------------------------------------------------------------------
 // wave helpers (64 lanes)
+// inclusive prefix sum over the wave's 64 lanes (every lane active): DPP row shifts 1, 2, 4, 8 scan
+// each 16-lane row, row broadcasts 15 and 31 carry the rows' totals (VALU only; round 5a: six
+// __shfl_up steps, each an LDS permute round trip)
 __device__ __forceinline__ int wave_incl_scan(int x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 into rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 into rows 2, 3
   return x;
+}
+
+// one DPP step of the argmax: take the (u, i) that `ctrl` brings in where it is larger (u greater, or
+// equal u and a smaller index); lanes outside row_mask bring in their own pair
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void argmax_dpp_step(double& u, int& i) {
+  const long long ub = __double_as_longlong(u);
+  const int lo = (int)(uint32_t)ub, hi = (int)(ub >> 32);
+  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xf, false);
+  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xf, false);
+  const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, ROW_MASK, 0xf, false);
+  const double ou = __longlong_as_double(((long long)ohi << 32) | (long long)(uint32_t)olo);
+  if (ou > u || (ou == u && oi < i)) {
+    u = ou;
+    i = oi;
+  }
+}
+
+// the wave's argmax of u with the first index among equals (every lane active); returned uniform
+__device__ __forceinline__ int wave_argmax_dpp(double u, int i) {
+  argmax_dpp_step<0xb1, 0xf>(u, i);    // quad_perm [1,0,3,2]
+  argmax_dpp_step<0x4e, 0xf>(u, i);    // quad_perm [2,3,0,1]
+  argmax_dpp_step<0x141, 0xf>(u, i);   // row_half_mirror: each 8-lane half-row
+  argmax_dpp_step<0x140, 0xf>(u, i);   // row_mirror: each 16-lane row
+  argmax_dpp_step<0x142, 0xa>(u, i);   // row_bcast:15 into rows 1, 3
+  argmax_dpp_step<0x143, 0xc>(u, i);   // row_bcast:31 into rows 2, 3: lane 63 holds the wave's
+  return __builtin_amdgcn_readlane(i, 63);
 }
 
 __device__ __forceinline__ BB dev_apply_code(const BB& b, int code) {
@@ -45,11 +75,21 @@ __device__ __forceinline__ BB dev_apply_code(const BB& b, int code) {
 // The rule tables (knight / king / pawn attacks, rays: 1,444 B) copied into the workgroup's LDS:
 // move generation looks them up per lane with lane-varying squares, which from the constant
 // bank are vector loads through the texture path (tools/select_stamps.py: 58% of k_select's
-// cycles went to move generation with the tables there).  Call with all lanes, then barrier.
+// cycles went to move generation with the tables there).  Call with the one 64-lane wave of a
+// 64-thread workgroup, then barrier.  All of a lane's loads are issued before its first LDS store:
+// round 5a's strided loop (stride blockDim.x) compiled to a remainder loop that waited for each
+// load in turn, six dependent round trips at the start of every k_select.
 __device__ __forceinline__ void load_rules_lds(RuleTables* s_rt) {
+  constexpr int NW = (int)(sizeof(RuleTables) / 4), PER = (NW + 63) / 64;
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&d_rules);
   uint32_t* dst = reinterpret_cast<uint32_t*>(s_rt);
-  for (int i = threadIdx.x; i < (int)(sizeof(RuleTables) / 4); i += blockDim.x) dst[i] = src[i];
+  const int lane = threadIdx.x & 63;
+  uint32_t v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) v[j] = lane + 64 * j < NW ? src[lane + 64 * j] : 0u;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (lane + 64 * j < NW) dst[lane + 64 * j] = v[j];
 }
 
 // LDS scratch of one wave's move generation
@@ -73,7 +113,7 @@ __device__ int wave_legal(const BB& b, uint32_t flags, const RuleTables& RT, Leg
   if (lane < NSQ && ((own >> lane) & 1u)) ps = pseudo_targets(b, lane, flags, RT);
   const int cnt = popc(ps);
   const int incl = wave_incl_scan(cnt);
-  const int nps = __shfl(incl, 63, 64);     // <= 15 * 15: own pieces x other squares
+  const int nps = __builtin_amdgcn_readlane(incl, 63);     // <= 15 * 15: own pieces x other squares
   if (nps > KMAX) return -1;                // (unreachable from legal play; keeps L.pm in bounds)
   int off = incl - cnt;
   for (uint32_t m = ps; m; m &= m - 1) L.pm[off++] = (uint16_t)(lane | (lsb(m) << 8));
@@ -96,19 +136,31 @@ __device__ int wave_legal(const BB& b, uint32_t flags, const RuleTables& RT, Leg
     }
     const int mincl = wave_incl_scan(mult);
     int o = total + mincl - mult;
-    total += __shfl(mincl, 63, 64);
+    total += __builtin_amdgcn_readlane(mincl, 63);
     if (total > KMAX) return -1;
     for (int r = 0; r < mult; ++r) L.raw[o++] = (uint16_t)code;
   }
   __syncthreads();
-  for (int j = lane; j < total; j += 64) {
-    const uint16_t c = L.raw[j];
+  if (total <= 64) {
+    // rank by code, then list index: lane j holds code j and reads the others with readlane (the
+    // loop index is uniform), not from LDS (round 5a: one dependent LDS read per code and lane)
+    const int c = lane < total ? (int)L.raw[lane] : 0xffff;
     int rank = 0;
     for (int i = 0; i < total; ++i) {
-      const uint16_t o = L.raw[i];
-      rank += (o < c) || (o == c && i < j);
+      const int o = __builtin_amdgcn_readlane(c, i);
+      rank += (o < c) || (o == c && i < lane);
     }
-    L.sorted[rank] = c;
+    if (lane < total) L.sorted[rank] = (uint16_t)c;
+  } else {
+    for (int j = lane; j < total; j += 64) {
+      const uint16_t c = L.raw[j];
+      int rank = 0;
+      for (int i = 0; i < total; ++i) {
+        const uint16_t o = L.raw[i];
+        rank += (o < c) || (o == c && i < j);
+      }
+      L.sorted[rank] = c;
+    }
   }
   __syncthreads();
   return total;
@@ -255,6 +307,31 @@ __device__ __forceinline__ uint32_t tree_find(const Trees& T, int t, const Pos& 
   return NONE;
 }
 
+// tree_find with its first probe done by the caller: v = the table's word at slot h (the position's
+// home slot), vp = the position of node v - 1 (read when v != 0)
+__device__ __forceinline__ uint32_t tree_find_first(const Trees& T, int t, const Pos& p, uint32_t h, uint32_t v,
+                                                    const Pos& vp, uint32_t* slot) {
+  if (v == 0) {
+    *slot = h;
+    return NONE;
+  }
+  if (pos_eq(vp, p)) return v - 1;
+  const uint32_t mask = (uint32_t)T.HC - 1;
+  const uint32_t* ht = T.hash + (size_t)t * T.HC;
+  const Pos* np = T.node_pos + (size_t)t * T.NC;
+  for (int probe = 1; probe < T.HC; ++probe) {
+    h = (h + 1) & mask;
+    const uint32_t w = ht[h];
+    if (w == 0) {
+      *slot = h;
+      return NONE;
+    }
+    if (pos_eq(np[w - 1], p)) return w - 1;
+  }
+  *slot = (uint32_t)T.HC;
+  return NONE;
+}
+
 // single lane; `n_nodes` = the tree's node count (read at kernel start: only this wave adds nodes)
 __device__ uint32_t tree_insert(const Trees& T, int t, const Pos& p, uint32_t slot, uint32_t n_nodes, int32_t* err) {
   if (n_nodes >= (uint32_t)T.NC) {
@@ -393,39 +470,59 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
   __shared__ LegalLds s_l;
   __shared__ RuleTables s_rt;
   const int g = blockIdx.x, lane = threadIdx.x;
+  // One round of loads for the game's words (the gates, agent, root, root-node hint, noise
+  // address, both tables' counters) and the rule tables.  Round 5a read the gates one behind
+  // another and the tree's counters behind the agent: five dependent round trips before the root's
+  // header, about 1.9 us each even on an idle chip (tools/select_stamps.py at 256 games).
+  // (the game's active byte read as part of its aligned word: a byte load went out, and was waited
+  // for, ahead of the other loads)
+  const bool act = ((reinterpret_cast<const uint32_t*>(D.gm.active)[g >> 2] >> (8 * (g & 3))) & 0xffu) != 0;
+  const uint32_t pend = defer ? D.lf.gnode[g] : NONE;
+  const int sc = defer ? D.gm.simc[g] : 0;
+  const int ag = D.gm.agent[g];
+  Pos pos = D.gm.root[g];
+  uint32_t n = D.gm.root_node[g];
+  const int64_t noff = D.gm.noise_off[g];
+  const int32_t njs = D.gm.noise_js[g], rnew = D.gm.root_new[g];
+  const uint2 nn2 = *reinterpret_cast<const uint2*>(D.tr.n_nodes + 2 * g);   // trees 2g, 2g + 1
+  const uint2 ne2 = *reinterpret_cast<const uint2*>(D.tr.n_edges + 2 * g);
+  load_rules_lds(&s_rt);
+  // the values are needed here, so every load above is issued before the gates branch (the
+  // compiler otherwise sinks each load into the branch that uses it, one round trip after another)
+  asm volatile("" ::"v"((uint32_t)act), "v"(pend), "v"(sc), "v"(ag), "v"(pos.sq[0]), "v"(pos.sq[1]), "v"(pos.sq[2]),
+               "v"(pos.sq[3]), "v"(pos.info), "v"(n), "v"(noff), "v"(njs), "v"(rnew), "v"(nn2.x), "v"(nn2.y),
+               "v"(ne2.x), "v"(ne2.y));
   if (!defer) {
     if (lane == 0) {
       D.lf.gnode[g] = NONE;
       D.lf.ghit[g] = 0;
     }
-    if (!D.gm.active[g]) return;
+    if (!act) return;
   } else {
     // deferred-tail play: the game's own next simulation, unless its last leaf is still pending
     // (deferred by k_leaf_compact) or it has started all of them.  A game's simulations run in
     // order, one at a time, exactly as in lockstep; only the wave each one runs in moves.
     if (lane == 0) D.lf.ghit[g] = 0;
-    if (!D.gm.active[g] || D.lf.gnode[g] != NONE) return;
-    const int s = D.gm.simc[g];
-    if (s >= D.pr.sims) return;
-    if (lane == 0) D.gm.simc[g] = s + 1;
-    sim = s;
+    if (!act || pend != NONE) return;
+    if (sc >= D.pr.sims) return;
+    if (lane == 0) D.gm.simc[g] = sc + 1;
+    sim = sc;
   }
 #ifdef MTAZ_NET_DIAG
   unsigned long long sel_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long sel_t0 = __builtin_amdgcn_s_memtime();
   unsigned long long sel_t = sel_t0;
 #endif
-  load_rules_lds(&s_rt);
   const Trees& T = D.tr;
-  const int t = 2 * g + D.gm.agent[g];
+  const int t = 2 * g + ag;
   const size_t nbase = (size_t)t * T.NC;
   const uint32_t ebase = (uint32_t)t * (uint32_t)T.EC;   // the tree's own edge region
   uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
   uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
-  const uint32_t n_nodes = T.n_nodes[t], n_edges = T.n_edges[t];
-  Pos pos = D.gm.root[g];
+  const uint32_t n_nodes = ag ? nn2.y : nn2.x, n_edges = ag ? ne2.y : ne2.x;
   int depth = 0;
-  uint32_t n = D.gm.root_node[g];
+  // this simulation's Dirichlet vector (read at the root only)
+  const double* noise = D.gm.noise + noff + (int64_t)(sim - rnew) * njs;
   // the hinted node's position and header in one round trip (the header is used only if the
   // position matches)
   const size_t nh = nbase + (n < (uint32_t)T.NC ? n : 0u);
@@ -438,8 +535,22 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
   __syncthreads();
   for (;;) {
     if (!linked) {
+      // The position's first probes in this tree's table, the game's other table (memo >= 1) and
+      // the batch memo (memo 2) go out in one round of loads, the probed slots' positions in the
+      // next (round 5a: each lookup behind the previous one, six round trips before an expansion
+      // that misses all three); a collision continues the probe sequence as tree_find does.
+      const uint32_t hp = pos_hash(pos), h0 = hp & ((uint32_t)T.HC - 1);
+      const bool memo1 = D.pr.memo != 0, memo2 = D.pr.memo >= 2 && D.bm.cap != 0;
+      const uint32_t v0 = T.hash[(size_t)t * T.HC + h0];
+      const uint32_t v1 = memo1 ? T.hash[(size_t)(t ^ 1) * T.HC + h0] : 0u;
+      const uint32_t hb = memo2 ? (hp & (D.bm.cap - 1)) : 0u;
+      const uint32_t bs = memo2 ? D.bm.state[hb] : 0u;
+      Pos bkey{}, p0{}, p1{};
+      if (memo2) bkey = D.bm.key[hb];
+      if (v0 != 0u) p0 = T.node_pos[nbase + v0 - 1];
+      if (v1 != 0u) p1 = T.node_pos[(size_t)(t ^ 1) * T.NC + v1 - 1];
       uint32_t slot;
-      n = tree_find(T, t, pos, &slot);
+      n = tree_find_first(T, t, pos, h0, v0, p0, &slot);
       SEL_T(1);
       if (n == NONE) {
         // ---- expansion (exp/agent.py:57-73) ----
@@ -455,21 +566,21 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
         const uint16_t* msrc_code = nullptr;
         const float* msrc_P = nullptr;
         uint8_t mkind = 0;   // 1 = the game's other table, 2 = the batch memo
-        if (D.pr.memo) {
+        if (memo1) {
           uint32_t s2;
-          m = tree_find(T, t ^ 1, pos, &s2);
+          m = tree_find_first(T, t ^ 1, pos, h0, v1, p1, &s2);
           if (m != NONE) {
             mkind = 1;
             mh = T.node_hdr[(size_t)(t ^ 1) * T.NC + m];
             msrc_code = T.e_code + mh.e0;
             msrc_P = T.e_P + mh.e0;
-          } else if (D.pr.memo >= 2) {
+          } else if (memo2) {
             const BatchMemo& B = D.bm;
             const uint32_t mask = B.cap - 1;
-            uint32_t h = pos_hash(pos) & mask;
+            uint32_t h = hb;
             for (uint32_t probe = 0; probe < MEMO_PROBES; ++probe, h = (h + 1) & mask) {
-              if (B.state[h] == 0u) break;
-              if (pos_eq(B.key[h], pos)) {
+              if ((probe ? B.state[h] : bs) == 0u) break;
+              if (pos_eq(probe ? B.key[h] : bkey, pos)) {
                 m = h;
                 mkind = 2;
                 mh = NodeHdr{0u, 0u, (uint32_t)B.k[h], B.v[h]};
@@ -539,8 +650,8 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
             else D.gm.root_node[g] = nn;
           }
         }
-        nn = __shfl(nn, 0, 64);
-        ne0 = __shfl(ne0, 0, 64);
+        nn = (uint32_t)__builtin_amdgcn_readlane((int)nn, 0);   // lane 0 decided (every lane active)
+        ne0 = (uint32_t)__builtin_amdgcn_readlane((int)ne0, 0);
         if (nn != NONE) {
           if (!term) {
             for (int c = lane; c < k; c += 64) {
@@ -584,11 +695,6 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
     }
     const double sq = D.pr.sqrt_tab[S];
     const bool root = depth == 0;
-    const double* noise = nullptr;
-    if (root) {
-      const int j = sim - D.gm.root_new[g];
-      noise = D.gm.noise + D.gm.noise_off[g] + (int64_t)j * D.gm.noise_js[g];
-    }
     double best_u = -__builtin_inf();
     int best_i = 0x7fffffff;
     uint32_t best_cc = 0;   // winner's code | linked child (the child index in a second word)
@@ -615,14 +721,14 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
       const double u = Q + tt / (1.0 + N);
       if (u > best_u) { best_u = u; best_i = c; best_cc = code; best_ch = child; }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ou = __shfl_xor(best_u, o, 64);
-      const int oi = __shfl_xor(best_i, o, 64);
-      const uint32_t occ = __shfl_xor(best_cc, o, 64), och = __shfl_xor(best_ch, o, 64);
-      if (ou > best_u || (ou == best_u && oi < best_i)) { best_u = ou; best_i = oi; best_cc = occ; best_ch = och; }
-    }
-    const int a = best_i;
+    // wave argmax of (u, first index) by DPP steps (quad permutes, half-row and row mirrors, row
+    // broadcasts 15 and 31: VALU only, the wave's winner in lane 63), then the winner's code and
+    // child read from the lane that held it (round 4: five ds_bpermute shuffles per butterfly step,
+    // six steps).  The order (u descending, index ascending) is total, so every reduction tree
+    // gives the butterfly's winner.
+    const int a = wave_argmax_dpp(best_u, best_i);
+    best_cc = (uint32_t)__builtin_amdgcn_readlane((int)best_cc, a & 63);
+    best_ch = (uint32_t)__builtin_amdgcn_readlane((int)best_ch, a & 63);
     if (depth >= D.gm.DMAX) {
       if (lane == 0) atomicOr(D.pr.err, ERR_DEPTH);
       return;
@@ -640,6 +746,18 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
   }
 }
 
+// a position as five words in registers (k_leaf_compact): i < 0 gives zeros
+__device__ __forceinline__ void load_pos_words(uint32_t (&w)[5], const Pos* __restrict__ src, int i) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(src + (i < 0 ? 0 : i));
+#pragma unroll
+  for (int f = 0; f < 5; ++f) w[f] = i < 0 ? 0u : q[f];
+}
+__device__ __forceinline__ void store_pos_words(Pos* __restrict__ dst, int i, const uint32_t (&w)[5]) {
+  uint32_t* q = reinterpret_cast<uint32_t*>(dst + i);
+#pragma unroll
+  for (int f = 0; f < 5; ++f) q[f] = w[f];
+}
+
 // The leaf batch: one workgroup; per chunk of 4,096 games thread i holds games 4i..4i+3 in registers
 // (their leaf, agent and position in one round of loads: loads placed after the stores would wait
 // for them), a block scan of the per-thread counts places its leaves.  Classic play lists the
@@ -652,6 +770,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
                                                        int cut, int round) {
   constexpr int PER = 4, NBK = 4;
   __shared__ int s_w[16];
+  __shared__ int s_w2[16][2];
   __shared__ int s_hits[2];
   __shared__ int s_bk[NBK];   // leaves per lag bucket (pass 1), then the bucket's next slot
   __shared__ int s_smax;
@@ -667,14 +786,14 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     const int g0 = tid * PER;
     uint32_t nd[PER];
     int ag[PER], sc[PER], bk[PER];
-    Pos ps[PER];
+    uint32_t ps[PER][5];   // positions as words (an array of Pos compiles to scratch copies)
     int hits = 0, bhits = 0, m = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const bool in = g0 + j < G;
       nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
       ag[j] = in ? D.gm.agent[g0 + j] : 0;
-      ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
+      load_pos_words(ps[j], D.lf.gpos, in ? g0 + j : -1);
       sc[j] = in ? D.gm.simc[g0 + j] - 1 : 0;
       const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
       hits += hk == 1;
@@ -685,63 +804,67 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     if (lane == 0) atomicMax(&s_smax, m);
     __syncthreads();
     const int smx = s_smax;
-    int cb[NBK] = {0, 0, 0, 0};
+    // the thread's leaves per bucket and its memo hits, 16-bit fields of three words (every field's
+    // block total is at most G <= 4,096, so no field carries into the next): one block scan of the
+    // three words places every bucket's leaves and gives the totals (round 5a: one block scan per
+    // bucket and a store pass per bucket, 22 us per launch)
+    uint32_t w01 = 0, w23 = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int lag = smx - sc[j];
       bk[j] = NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
-#pragma unroll
-      for (int q = 0; q < NBK; ++q) cb[q] += nd[j] != NONE && bk[j] == q;
-    }
-#pragma unroll
-    for (int q = 0; q < NBK; ++q) {
-      int x = cb[q];
-      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-      if (lane == 0 && x) atomicAdd(&s_bk[q], x);
-    }
-    __syncthreads();
-    int first[NBK], total = 0;
-#pragma unroll
-    for (int q = 0; q < NBK; ++q) {
-      first[q] = total;
-      total += s_bk[q];
-    }
-#pragma unroll
-    for (int q = 0; q < NBK; ++q) {
-      const int incl = wave_incl_scan(cb[q]);
-      if (lane == 63) s_w[w] = incl;
-      __syncthreads();
-      int slot = first[q] + incl - cb[q];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) slot += i < w ? s_w[i] : 0;
-      __syncthreads();   // s_w is rewritten by the next bucket's scan
-#pragma unroll
-      for (int j = 0; j < PER; ++j) {
-        if (nd[j] != NONE && bk[j] == q) {
-          const int g = g0 + j;
-          D.lf.game[slot] = g;
-          D.lf.tree[slot] = 2 * g + ag[j];
-          D.lf.node[slot] = nd[j];
-          D.lf.pos[slot] = ps[j];
-          ++slot;
-        }
+      if (nd[j] != NONE) {
+        const uint32_t one = 1u << (16 * (bk[j] & 1));
+        if (bk[j] < 2) w01 += one;
+        else w23 += one;
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      hits += __shfl_xor(hits, o, 64);
-      bhits += __shfl_xor(bhits, o, 64);
+    const uint32_t wh = (uint32_t)hits | ((uint32_t)bhits << 16);
+    const uint32_t i01 = (uint32_t)wave_incl_scan((int)w01), i23 = (uint32_t)wave_incl_scan((int)w23);
+    const uint32_t ih = (uint32_t)wave_incl_scan((int)wh);
+    if (lane == 63) {
+      s_w[w] = (int)i01;
+      s_w2[w][0] = (int)i23;
+      s_w2[w][1] = (int)ih;
     }
-    if (lane == 0 && hits) atomicAdd(&s_hits[0], hits);
-    if (lane == 0 && bhits) atomicAdd(&s_hits[1], bhits);
     __syncthreads();
+    uint32_t p01 = i01 - w01, p23 = i23 - w23, t01 = 0, t23 = 0, th = 0;   // exclusive prefixes, totals
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t x01 = (uint32_t)s_w[i], x23 = (uint32_t)s_w2[i][0];
+      p01 += i < w ? x01 : 0u;
+      p23 += i < w ? x23 : 0u;
+      t01 += x01;
+      t23 += x23;
+      th += (uint32_t)s_w2[i][1];
+    }
+    const int tot0 = (int)(t01 & 0xffffu), tot1 = (int)(t01 >> 16), tot2 = (int)(t23 & 0xffffu);
+    const int total = tot0 + tot1 + tot2 + (int)(t23 >> 16);
+    int sb[NBK] = {(int)(p01 & 0xffffu), tot0 + (int)(p01 >> 16), tot0 + tot1 + (int)(p23 & 0xffffu),
+                   tot0 + tot1 + tot2 + (int)(p23 >> 16)};   // the thread's next slot in each bucket
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (nd[j] != NONE) {
+        int slot = sb[0];
+#pragma unroll
+        for (int q = 1; q < NBK; ++q) slot = bk[j] == q ? sb[q] : slot;
+#pragma unroll
+        for (int q = 0; q < NBK; ++q) sb[q] += bk[j] == q;
+        const int g = g0 + j;
+        D.lf.game[slot] = g;
+        D.lf.tree[slot] = 2 * g + ag[j];
+        D.lf.node[slot] = nd[j];
+        store_pos_words(D.lf.pos, slot, ps[j]);
+      }
+    }
     if (tid == 0) {
       const int rem = round > 0 ? total % round : 0;
       const int n = (cut && round > 0 && total >= round && (cut == 2 || rem <= 3 * (round / 4))) ? total - rem : total;
       *D.lf.count = n;
       if (count_log) {
         count_log[0] = n;
-        count_log[1] = s_hits[0];
-        count_log[2] = s_hits[1];
+        count_log[1] = (int)(th & 0xffffu);
+        count_log[2] = (int)(th >> 16);
       }
     }
     return;
@@ -791,13 +914,13 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     const int g0 = c0 + tid * PER;
     uint32_t nd[PER];
     int ag[PER], bk[PER];
-    Pos ps[PER];
+    uint32_t ps[PER][5];   // positions as words (an array of Pos compiles to scratch copies)
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const bool in = g0 + j < G;
       nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
       ag[j] = in ? D.gm.agent[g0 + j] : 0;
-      ps[j] = in ? D.lf.gpos[g0 + j] : Pos{};
+      load_pos_words(ps[j], D.lf.gpos, in ? g0 + j : -1);
       bk[j] = (in && nd[j] != NONE) ? bucket(g0 + j) : 0;
       const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
       hits += hk == 1;
@@ -826,7 +949,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
           D.lf.game[slot] = g;
           D.lf.tree[slot] = 2 * g + ag[j];
           D.lf.node[slot] = nd[j];
-          D.lf.pos[slot] = ps[j];
+          store_pos_words(D.lf.pos, slot, ps[j]);
           ++slot;
         }
       }
@@ -914,16 +1037,56 @@ int diag_select_stamps(unsigned long long* out8, int reset) {
 // Leaf expansion finish + backup (exp/agent.py:68-72): store P, back up v.  One wave per leaf:
 // lanes copy the priors and update one path level each.
 __global__ __launch_bounds__(256) void k_backup(Dev D) {
+#pragma clang fp contract(off)
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= *D.lf.count) return;
   const Trees& T = D.tr;
   const int g = D.lf.game[i], t = D.lf.tree[i];
   const uint32_t n = D.lf.node[i];
   const size_t nbase = (size_t)t * T.NC;
+  const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
+  const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
+  // one round of loads for what depends only on the leaf's slot and game: its header, value and
+  // first 64 priors, the path length and the lane's path level (read before the length is known:
+  // a level past it is not used), so that the backup's loads go out ahead of the memo's CAS chain
+  // (round 5a: header, priors, memo, then the path, each behind the previous)
   const NodeHdr hd = T.node_hdr[nbase + n];
+  const float vf = D.lf.v[i];
+  const int depth = D.gm.path_len[g];
+  const bool lvl = lane < D.gm.DMAX;
+  const uint32_t pe0 = lvl ? pe[lane] : 0u, pn0 = lvl ? pn[lane] : 0u;
+  const float P0 = D.lf.P[(size_t)i * KMAX + lane];
+  const Pos p = D.lf.pos[i];
   const int k = hdr_k(hd);
-  for (int c = lane; c < k; c += 64) T.e_P[(size_t)hd.e0 + c] = D.lf.P[(size_t)i * KMAX + c];
-  if (lane == 0) T.node_hdr[nbase + n].tval = D.lf.v[i];   // kept for the leaf memo (Params::memo)
+  {
+    // exp/agent.py:47-52 as backup_path, level d = lane from the loads above, then any level >= 64
+    const double v = (double)vf;
+    if (lane < depth) {
+      const double vd = ((depth - lane) & 1) ? -v : v;
+      const uint32_t Ni = T.e_N[pe0];
+      const double N = (double)Ni;
+      const double Q = T.e_Q[pe0];
+      const double prod = N * Q;
+      const double num = prod + vd;
+      T.e_Q[pe0] = num / (N + 1.0);
+      T.e_N[pe0] = Ni + 1;
+      T.node_hdr[nbase + pn0].sumN += 1;
+    }
+    for (int d = lane + 64; d < depth; d += 64) {
+      const double vd = ((depth - d) & 1) ? -v : v;
+      const size_t e = pe[d];
+      const uint32_t Ni = T.e_N[e];
+      const double N = (double)Ni;
+      const double Q = T.e_Q[e];
+      const double prod = N * Q;
+      const double num = prod + vd;
+      T.e_Q[e] = num / (N + 1.0);
+      T.e_N[e] = Ni + 1;
+      T.node_hdr[nbase + pn[d]].sumN += 1;
+    }
+  }
+  for (int c = lane; c < k; c += 64) T.e_P[(size_t)hd.e0 + c] = c < 64 ? P0 : D.lf.P[(size_t)i * KMAX + c];
+  if (lane == 0) T.node_hdr[nbase + n].tval = vf;   // kept for the leaf memo (Params::memo)
   if (D.pr.memo >= 2 && D.bm.cap && k <= MEMO_K) {
     // batch memo insert: claim a slot (0 -> 1), write, publish (-> 2); a slot another leaf of this
     // launch claimed is passed over (at worst a position is kept twice, with identical results).
@@ -932,7 +1095,6 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
     // this launch a prober may see state 2 before the key: it then passes over the slot or, on a
     // stale key equal to its own, skips the insert (a memo miss later, never a wrong entry).
     const BatchMemo& B = D.bm;
-    const Pos p = D.lf.pos[i];
     uint32_t slot = NONE;
     if (lane == 0) {
       const uint32_t mask = B.cap - 1;
@@ -946,23 +1108,21 @@ __global__ __launch_bounds__(256) void k_backup(Dev D) {
         if (st == 2u && pos_eq(B.key[h], p)) break;
       }
     }
-    slot = __shfl(slot, 0, 64);
+    slot = (uint32_t)__builtin_amdgcn_readlane((int)slot, 0);
     if (slot != NONE) {
       for (int c = lane; c < k; c += 64) {
         B.codes[(size_t)slot * MEMO_K + c] = T.e_code[(size_t)hd.e0 + c];
-        B.P[(size_t)slot * MEMO_K + c] = D.lf.P[(size_t)i * KMAX + c];
+        static_assert(MEMO_K <= 64, "a memo entry's priors are the lanes' first priors");
+        B.P[(size_t)slot * MEMO_K + c] = P0;   // c = lane
       }
       if (lane == 0) {
         B.key[slot] = p;
-        B.v[slot] = D.lf.v[i];
+        B.v[slot] = vf;
         B.k[slot] = (uint16_t)k;
         B.state[slot] = 2u;
       }
     }
   }
-  const uint32_t* pn = D.gm.path_node + (size_t)g * D.gm.DMAX;
-  const uint32_t* pe = D.gm.path_edge + (size_t)g * D.gm.DMAX;
-  backup_path(T, t, pn, pe, D.gm.path_len[g], (double)D.lf.v[i], lane);
   if (lane == 0) D.lf.gnode[g] = NONE;   // evaluated: no longer pending (deferred-tail play)
 }
 
