@@ -508,9 +508,21 @@ def main():
         eng36.set_sync_mode(sync_mode)
         eng36.set_defer(args.defer)
         eng36.evaluate(np.stack([start_position()] * 8))
-        dt3, tot3, prec3 = timed(eng36, 1, f'{args.default_sims} sims')
-        at_default = {'sims_per_move': args.default_sims, 'value': G * world / dt3, 'unit': 'games/s', 'steps': 1,
-                      'ms_per_step': dt3 * 1e3, 'roofline': kernel_roofline(tot3, prec3), **counters(tot3, dt3, G * world)}
+        # a second step when it and the CPU legs still to come (all cores: the GPU's sims, 36 and 32
+        # on 3 seeds at ~0.31 s per sim per game on 16 cores, profiles/r05/final) end inside the
+        # budget (the 36-sims point for at least 2 steps if the budget allows)
+        cpu_rest = 0.0
+        if world == 1 and not args.no_cpu_baseline:
+            n_seeds = 3 if args.cpu_plan == 'full' else 1
+            cpu_rest = n_seeds * 0.31 * (sims + args.default_sims + 32) * 16 / max(1, host_cores()['usable']) + 10
+        step36 = step_s * args.default_sims / sims * 1.15
+        n36 = 2 if agree_max(elapsed() + 2 * step36 + 5 + cpu_rest) <= args.time_budget else 1
+        if n36 == 1:
+            budget['skipped'].append({'leg': f'second {args.default_sims}-sims step', 'estimate_s': round(step36, 1)})
+        dt3, tot3, prec3 = timed(eng36, n36, f'{args.default_sims} sims')
+        at_default = {'sims_per_move': args.default_sims, 'value': G * world * n36 / dt3, 'unit': 'games/s', 'steps': n36,
+                      'ms_per_step': dt3 * 1e3 / n36, 'roofline': kernel_roofline(tot3, prec3),
+                      **counters(tot3, dt3, G * world * n36)}
         eng36.close()
 
     # secondary line (opt-in, --secondary): one more timed step on the other fused network (k_net_z,
