@@ -508,13 +508,15 @@ def main():
         eng36.set_sync_mode(sync_mode)
         eng36.set_defer(args.defer)
         eng36.evaluate(np.stack([start_position()] * 8))
-        # a second step when it and the CPU legs still to come (all cores: the GPU's sims, 36 and 32
-        # on 3 seeds at ~0.31 s per sim per game on 16 cores, profiles/r05/final) end inside the
-        # budget (the 36-sims point for at least 2 steps if the budget allows)
+        # a second step when it and the CPU legs still to come end inside the budget by cpu_baseline's
+        # own estimates (the value leg at 0.35 s per sim per game on 16 cores, the others 1.25x that),
+        # so that the step never costs a CPU leg (the 36-sims point for at least 2
+        # steps if the budget allows; at the driver's --steps 20 it does not: profiles/r05/final2)
         cpu_rest = 0.0
         if world == 1 and not args.no_cpu_baseline:
             n_seeds = 3 if args.cpu_plan == 'full' else 1
-            cpu_rest = n_seeds * 0.31 * (sims + args.default_sims + 32) * 16 / max(1, host_cores()['usable']) + 10
+            others = (args.default_sims + 32) if args.cpu_plan == 'full' else args.default_sims
+            cpu_rest = n_seeds * 0.35 * (sims + 1.25 * others) * 16 / max(1, host_cores()['usable']) + 15
         step36 = step_s * args.default_sims / sims * 1.15
         n36 = 2 if agree_max(elapsed() + 2 * step36 + 5 + cpu_rest) <= args.time_budget else 1
         if n36 == 1:
