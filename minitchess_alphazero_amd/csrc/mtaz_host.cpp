@@ -2011,9 +2011,14 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     const size_t need = (size_t)std::max<int64_t>(K, 1) * h->sims;
     ECHK(ensure_noise(h, need));   // (mtaz_move_begin synchronised the stream)
     if (need > h->noise_host_cap) {
+      // grown geometrically, as the device buffer: pinning a fresh buffer costs ~4 ms, and the
+      // legal counts grow over a game's first moves (round 5a regrew it on about twenty of them)
+      const size_t cap = std::max(need, 2 * h->noise_host_cap);
       if (h->noise_host) HIPCHK(hipHostFree(h->noise_host));
-      HIPCHK(hipHostMalloc(&h->noise_host, need * 8, hipHostMallocDefault));
-      h->noise_host_cap = need;
+      h->noise_host = nullptr;
+      h->noise_host_cap = 0;
+      HIPCHK(hipHostMalloc(&h->noise_host, cap * 8, hipHostMallocDefault));
+      h->noise_host_cap = cap;
     }
     for (int g = 0; g < G; ++g) js[g] = (int32_t)K;
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs.data(), G * 8, hipMemcpyHostToDevice, h->stream));
