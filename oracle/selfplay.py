@@ -79,11 +79,15 @@ class _MCInit:
 
 
 def play_games(evaluator, num_games, sims, seed_base=0, cpuct=1, tau_change=6, cast_mode=2,
-               record=None, stats=None, trace=None):
+               record=None, stats=None, trace=None, start_fen=None):
     """Play `num_games` seeded self-play games; return the list of episode records.
     `evaluator` may be a pair: agent 0 (first mover, exp/agent.py:11-14) uses the first, agent 1
     the second (the arena of the commented exp/learner.py:97-145)."""
     env = MinitChessEnvironment()
+    if start_fen is not None:
+        # every episode from start_fen (exp/environment.py new_episode's fen argument)
+        base_new = env.new_episode
+        env.new_episode = lambda fen=None: base_new(fen or start_fen)
     rng = np.random.RandomState(seed_base)
     evs = tuple(evaluator) if isinstance(evaluator, (tuple, list)) else (evaluator, evaluator)
     agents = [SimpleAlphaZeroAgent(env, SimpleAlphaZeroPolicy(evs[i]), sims, cpuct, tau_change, rng=rng,

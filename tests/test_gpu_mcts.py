@@ -76,6 +76,34 @@ def test_trees_bit_exact_vs_oracle(memo, spill):
         assert dst['nn_evals'] == ref_evals
 
 
+def test_long_legal_lists_trees_bit_exact():
+    """Roots with 70-73 legal moves (conftest.LONG_LIST_FENS): move generation ranks more codes
+    than a wave has lanes (wave_legal's LDS fallback) and the PUCT argmax holds two children per
+    lane; moves, rewards and both final tables equal the oracle's (SyntheticEvaluator, 24 sims)."""
+    from conftest import LONG_LIST_FENS
+    from oracle.mcts import SyntheticEvaluator
+    from oracle import selfplay
+    ev = SyntheticEvaluator(salt=5)
+    seeds = [201 + i for i in range(len(LONG_LIST_FENS))]
+    eng = _engine(len(seeds), 24)
+    trees = []
+    recs, _ = drive_engine(eng, len(seeds), 24, seeds, evaluator=ev, start_fen=LONG_LIST_FENS, trees_out=trees)
+    for g, (s, fen) in enumerate(zip(seeds, LONG_LIST_FENS)):
+        st = {}
+        ref = selfplay.play_games(ev, 1, 24, seed_base=s, stats=st, start_fen=fen)[0]
+        assert len(recs[g][0]['legal_moves']) > 64, fen
+        assert compare_records(recs[g], ref)[2] is None, fen
+        assert [r['reward'] for r in recs[g]] == [r['reward'] for r in ref], fen
+        for agent in (0, 1):
+            mine, theirs = trees[g][agent], st['trees'][0][agent]
+            assert mine['visited'] == theirs['visited'], fen
+            assert set(mine['Q']) == set(theirs['Q']), fen
+            for f in theirs['Q']:
+                assert mine['legal_moves'][f] == list(theirs['legal_moves'][f]), f
+                assert np.array_equal(mine['Q'][f], theirs['Q'][f]), f
+                assert np.array_equal(mine['N'][f], theirs['N'][f]), f
+
+
 def _net(kind):
     """seed0: torch.manual_seed(0); Network().  stress: the round-3 stress checkpoint (trunk
     activations in the thousands; its k_net_y stored-units exponents leave 0 on a few positions).

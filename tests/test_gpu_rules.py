@@ -4,7 +4,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import LONG_LIST_FENS, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -23,7 +23,7 @@ def _positions(n, seed=5):
             out.append(b.fen())
             if b.result() != '*':
                 break
-    return out[:n] + [f['fen'] for f in load_golden('encoder')]
+    return out[:n] + [f['fen'] for f in load_golden('encoder')] + LONG_LIST_FENS
 
 
 def test_legal_batch_kernel_matches_oracle():

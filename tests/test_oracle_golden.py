@@ -204,3 +204,18 @@ def test_oracle_global_stream_two_episodes():
     st = rng.get_state()
     assert hashlib.sha256(st[1].tobytes()).hexdigest() == fx['rng_after']['key_sha256']
     assert int(st[2]) == fx['rng_after']['pos']
+
+
+def test_long_list_positions_exceed_a_wave():
+    """conftest.LONG_LIST_FENS keep their purpose: more legal moves than a wave has lanes, with
+    promotion duplicates in two of them, and a game still to play."""
+    from conftest import LONG_LIST_FENS
+    from oracle import rules
+    from oracle.environment import MinitChessEpisode
+    distinct = []
+    for f in LONG_LIST_FENS:
+        legal = MinitChessEpisode(f).get_legal_moves()
+        assert len(legal) > 64, f
+        assert rules.Board(f).result() == '*', f
+        distinct.append(len(set(legal)) < len(legal))
+    assert sum(distinct) >= 2
