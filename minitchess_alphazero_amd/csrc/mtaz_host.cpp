@@ -633,6 +633,20 @@ struct mtaz_engine {
   size_t noise_cap = 0;
   double* noise_host = nullptr;         // pinned staging of mtaz_play's draw-major noise
   size_t noise_host_cap = 0;
+  // pinned staging of mtaz_play's per-move transfers (ensure_play_pinned) and of check_err's flag
+  // word: copies to and from pageable memory are staged and synchronous, one round trip each
+  // (round 5a: ~13 of them per move, 20-40 us apart in the trace)
+  struct PlayPinned {
+    uint32_t* roots[2] = {nullptr, nullptr};   // double-buffered: the next move's states arrive
+    uint8_t* active[2] = {nullptr, nullptr};   // while the host still reads this move's
+    int32_t *agents = nullptr, *outcome = nullptr, *root_k = nullptr, *root_new = nullptr, *actions = nullptr;
+    int32_t* js = nullptr;
+    int64_t* offs = nullptr;
+    uint16_t* codes = nullptr;
+    uint32_t* visits = nullptr;
+  } pin;
+  void* pin_block = nullptr;
+  int32_t* err_host = nullptr;
   std::vector<int32_t> last_root_k;     // root legal counts of the last mtaz_move_begin
   std::vector<MTState> rng;
   std::vector<GameRec> rec;
@@ -678,6 +692,8 @@ struct mtaz_engine {
     for (mtaz_engine* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     if (noise_host) (void)hipHostFree(noise_host);
+    if (pin_block) (void)hipHostFree(pin_block);
+    if (err_host) (void)hipHostFree(err_host);
     for (auto e : ev) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : edge_allocs) (void)hipFree(p);
@@ -900,8 +916,10 @@ static hipError_t stream_wait(mtaz_engine* h) {
 // batch; there ERR_ZRANGE (k_net_z's per-workgroup exponent left 0) is an error, elsewhere a note.
 static int check_err(mtaz_engine* h, bool memo_path = true) {
   int32_t e = 0;
-  HIPCHK(hipMemcpyAsync(&e, h->d.pr.err, 4, hipMemcpyDeviceToHost, h->stream));
+  if (!h->err_host) HIPCHK(hipHostMalloc(&h->err_host, 4, hipHostMallocDefault));
+  HIPCHK(hipMemcpyAsync(h->err_host, h->d.pr.err, 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(stream_wait(h));
+  e = *h->err_host;
   if (e) {
     HIPCHK(hipMemsetAsync(h->d.pr.err, 0, 4, h->stream));
     if ((e & ERR_ZRANGE) && !(memo_path && h->d.pr.memo >= 1)) e &= ~ERR_ZRANGE;
@@ -1932,6 +1950,36 @@ static int play_groups(mtaz_engine* h) {
   return 0;
 }
 
+// the pinned per-move buffers of mtaz_play, one block for the engine's games
+static int ensure_play_pinned(mtaz_engine* h) {
+  if (h->pin_block) return 0;
+  const size_t G = (size_t)h->G;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+  const size_t o_r0 = take(G * 20), o_r1 = take(G * 20), o_a0 = take(G), o_a1 = take(G), o_ag = take(G * 4),
+               o_oc = take(G * 4), o_rk = take(G * 4), o_rn = take(G * 4), o_ac = take(G * 4), o_js = take(G * 4),
+               o_of = take(G * 8), o_co = take(G * KMAX * 2), o_vi = take(G * KMAX * 4);
+  void* q = nullptr;
+  HIPCHK(hipHostMalloc(&q, off, hipHostMallocDefault));
+  h->pin_block = q;
+  char* b = (char*)q;
+  auto& P = h->pin;
+  P.roots[0] = (uint32_t*)(b + o_r0);
+  P.roots[1] = (uint32_t*)(b + o_r1);
+  P.active[0] = (uint8_t*)(b + o_a0);
+  P.active[1] = (uint8_t*)(b + o_a1);
+  P.agents = (int32_t*)(b + o_ag);
+  P.outcome = (int32_t*)(b + o_oc);
+  P.root_k = (int32_t*)(b + o_rk);
+  P.root_new = (int32_t*)(b + o_rn);
+  P.actions = (int32_t*)(b + o_ac);
+  P.js = (int32_t*)(b + o_js);
+  P.offs = (int64_t*)(b + o_of);
+  P.codes = (uint16_t*)(b + o_co);
+  P.visits = (uint32_t*)(b + o_vi);
+  return 0;
+}
+
 extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
   if (n_games > h->G || n_games <= 0) return set_err(MTAZ_E_CAPACITY, "n_games=%d (engine has %d)", n_games, h->G);
@@ -1970,14 +2018,18 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->wave = 0;
   h->n_played = n_games;
 
-  std::vector<uint8_t> active(G);
-  std::vector<int32_t> agents(G), outcome_v(G), root_k(G), root_new(G), actions(G, 0);
-  std::vector<uint32_t> roots((size_t)G * 5);
-  std::vector<int64_t> offs(G);
-  std::vector<int32_t> js(G);
-  std::vector<uint16_t> codes((size_t)G * KMAX);
-  std::vector<uint32_t> visits((size_t)G * KMAX);
-  ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
+  ECHK(ensure_play_pinned(h));
+  auto& PP = h->pin;
+  int cur = 0;   // PP.roots[cur] / PP.active[cur]: this move's game states
+  uint32_t* roots = PP.roots[0];
+  uint8_t* active = PP.active[0];
+  int32_t *agents = PP.agents, *outcome_v = PP.outcome, *root_k = PP.root_k, *root_new = PP.root_new;
+  int32_t *actions = PP.actions, *js = PP.js;
+  int64_t* offs = PP.offs;
+  uint16_t* codes = PP.codes;
+  uint32_t* visits = PP.visits;
+  for (int g = 0; g < G; ++g) actions[g] = 0;
+  ECHK(mtaz_get_games(h, roots, agents, active, outcome_v));
   double rng_ms = 0, sync_ms = 0, choice_ms = 0, gap_ms = 0;
   double t_gap = -1;   // when the last move's root visit counts reached the host
   int moves = 0;
@@ -1995,7 +2047,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
       activate_slot(h, h->agent_slot[a]);
     }
     double ts = now_ms();
-    ECHK(mtaz_move_begin(h, root_k.data(), root_new.data()));
+    ECHK(mtaz_move_begin(h, root_k, root_new));
     sync_ms += now_ms() - ts;
     // Dirichlet draws: sims - root_new vectors of size k per active game, draw-major (draw j of
     // every game in one block of K = sum k), generated and uploaded in chunks of NCH draws so
@@ -2021,8 +2073,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
       h->noise_host_cap = cap;
     }
     for (int g = 0; g < G; ++g) js[g] = (int32_t)K;
-    HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs.data(), G * 8, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js.data(), G * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs, G * 8, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js, G * 4, hipMemcpyHostToDevice, h->stream));
     // chunks [0, 1), [1, 3), [3, 7), [7, 15), [15, 23), ...: the GPU starts after one draw per game,
     // and each later chunk is drawn while the previous chunk's simulations run.  The chunks double
     // up to 8 draws so that a chunk's draws never take longer than the simulations they overlap:
@@ -2080,16 +2132,16 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (int g = 0; g < G; ++g)
       if (active[g]) kmx = std::max(kmx, root_k[g]);
     ts = now_ms();
-    ECHK(mtaz_move_end(h, codes.data(), visits.data(), nullptr, kmx));
+    ECHK(mtaz_move_end(h, codes, visits, nullptr, kmx));
     sync_ms += now_ms() - ts;
     t_gap = now_ms();
-    // action selection (exp/agent.py:110-119) + records (exp/callbacks.py:40-47)
+    // action selection (exp/agent.py:110-119)
     tr = now_ms();
     parallel_for(G, h->host_threads, [&](int g) {
       if (!active[g]) return;
       const int k = root_k[g];
-      const uint16_t* c = codes.data() + (size_t)g * kmx;
-      const uint32_t* v = visits.data() + (size_t)g * kmx;
+      const uint16_t* c = codes + (size_t)g * kmx;
+      const uint32_t* v = visits + (size_t)g * kmx;
       double pi[KMAX];
       double sum = 0;
       for (int i = 0; i < k; ++i) sum += (double)v[i];
@@ -2107,13 +2159,28 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
         idx = maxima[legacy_randint(h->rng[g], m)];
       }
       actions[g] = c[idx];
-      h->rec[g].add(pos_in(&roots[5 * g]), c[idx], c, v, k);
     });
     rng_ms += now_ms() - tr;
     choice_ms += now_ms() - tr;
+    // the actions applied on the GPU and the next states on their way back while the host appends
+    // this move's records (exp/callbacks.py:40-47) from this move's buffers
     ts = now_ms();
-    ECHK(mtaz_apply(h, actions.data()));
-    ECHK(mtaz_get_games(h, roots.data(), agents.data(), active.data(), outcome_v.data()));
+    const int nxt = cur ^ 1;
+    HIPCHK(hipMemcpyAsync(h->d_actions, actions, G * 4, hipMemcpyHostToDevice, h->stream));
+    launch_apply(h->d, h->d_actions, h->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(PP.roots[nxt], h->d.gm.root, (size_t)G * sizeof(Pos), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(agents, h->d.gm.agent, G * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(PP.active[nxt], h->d.gm.active, G, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(outcome_v, h->d.gm.outcome, G * 4, hipMemcpyDeviceToHost, h->stream));
+    parallel_for(G, h->host_threads, [&](int g) {
+      if (!active[g]) return;
+      h->rec[g].add(pos_in(&roots[5 * g]), actions[g], codes + (size_t)g * kmx, visits + (size_t)g * kmx, root_k[g]);
+    });
+    ECHK(check_err(h));   // (synchronises the stream: the apply's flags and the states are in)
+    cur = nxt;
+    roots = PP.roots[cur];
+    active = PP.active[cur];
     sync_ms += now_ms() - ts;
     h->stats[ST_SIMS] += (double)n_active * h->sims;
     ++moves;
