@@ -68,6 +68,14 @@ double mtaz_rng_double(void* state);                                   /* random
 void mtaz_rng_dirichlet(void* state, double alpha, int k, double* out); /* dirichlet([a]*k)  */
 int64_t mtaz_rng_choice_p(void* state, const double* p, int k);        /* choice(k, p=p)    */
 int64_t mtaz_rng_randint(void* state, int64_t m);                      /* choice(m)         */
+/* The device build of the same generator (mtaz_play's default, mtaz_set_rng_device): stream s =
+ * RandomState(seeds[s]) draws n_vec dirichlet([alpha] * ks[s]) vectors (0 < alpha < 1), written as
+ * rows of ks[s] doubles, stream after stream, into out (host memory), then one random_sample() into
+ * tail[s].  Runs the kernels' own sampler code (csrc/mtaz_rng.hip: MT19937 words in LDS, 64 gamma
+ * attempts per wavefront, glibc's log/pow ported in csrc/glibc_math.h).  Replaces the host draws of
+ * exp/agent.py:82 (np.random.dirichlet). */
+int mtaz_rng_dirichlet_device(int device, const uint32_t* seeds, const int32_t* ks, int n_streams, int n_vec,
+                              double alpha, double* out, double* tail);
 
 /* ---- batched device kernels (minimum slice) ------------------------------------------- */
 /* Per position: sorted legal codes (KMAX=256 per row), count, 554-bit mask (18 words),
@@ -158,6 +166,14 @@ int mtaz_set_sync_mode(mtaz_engine* h, int mode);
  * draws and network results, so games, tables and records are identical in both modes; only the
  * wave each simulation runs in moves.  The fine-grained API (mtaz_sim_select ...) is unaffected. */
 int mtaz_set_defer(mtaz_engine* h, int mode);
+/* Where mtaz_play runs numpy's legacy RNG (exp/agent.py:82 Dirichlet noise, :114-118 action choice):
+ * 1 (default) = on the device: per-game MT19937 state in HBM, each move's Dirichlet draws in one
+ * launch (k_noise: one wavefront per game, 64 gamma attempts at once) and the action choice in
+ * another (k_choose); 0 = on the host (C++ MT19937 / legacy gamma / choice with glibc's log and pow,
+ * drawn in chunks that overlap the simulations).  Both give every game's RandomState(seed_base + g)
+ * stream draw for draw, so games are identical.  The device sampler covers 0 < dir_alpha < 1 (the
+ * reference's 0.6); other alphas run on the host. */
+int mtaz_set_rng_device(mtaz_engine* h, int on);
 /* per-wave log of the last mtaz_play (up to max_waves): out[3 * w + 0] leaves evaluated,
  * [+1] game-memo hits, [+2] batch-memo hits; returns the number of waves written */
 int mtaz_wave_log(mtaz_engine* h, int32_t* out, int max_waves);

@@ -38,6 +38,7 @@ SIGNATURES = {
     'mtaz_rng_dirichlet': (None, [c_void_p, c_double, c_int, P_f64]),
     'mtaz_rng_choice_p': (c_int64, [c_void_p, P_f64, c_int]),
     'mtaz_rng_randint': (c_int64, [c_void_p, c_int64]),
+    'mtaz_rng_dirichlet_device': (c_int, [c_int, P_u32, P_i32, c_int, c_int, c_double, P_f64, P_f64]),
     'mtaz_legal_batch': (c_int, [c_int, c_void_p, c_int, c_uint32, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'mtaz_encode_batch': (c_int, [c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     'mtaz_replay_put': (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
@@ -59,6 +60,7 @@ SIGNATURES = {
     'mtaz_set_host_threads': (c_int, [c_void_p, c_int]),
     'mtaz_set_sync_mode': (c_int, [c_void_p, c_int]),
     'mtaz_set_defer': (c_int, [c_void_p, c_int]),
+    'mtaz_set_rng_device': (c_int, [c_void_p, c_int]),
     'mtaz_wave_log': (c_int, [c_void_p, P_i32, c_int]),
     'mtaz_set_net_variant': (c_int, [c_void_p, c_int]),
     'mtaz_set_pipeline': (c_int, [c_void_p, c_int]),

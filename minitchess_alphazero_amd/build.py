@@ -37,10 +37,13 @@ SOURCES = [
     # is compiled into the diagnostic library alone
     ('mtaz_net16_r3.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000', 'DIAG_ONLY']),
     ('mtaz_net8.hip', ['-O3', '-mllvm', '-pragma-unroll-threshold=1000000']),
+    # numpy's legacy RNG on the device (k_noise, k_choose; glibc's log/pow ported in glibc_math.h,
+    # every FMA explicit, no contraction)
+    ('mtaz_rng.hip', ['-O3', '-ffp-contract=off', '-fno-fast-math']),
     ('mtaz_host.cpp', ['-O2', '-ffp-contract=off', '-fno-fast-math']),
     ('mtaz_wire.cpp', ['-O2']),
 ]
-HEADERS = ['rules.h', 'engine.h', 'net_common.h']
+HEADERS = ['rules.h', 'engine.h', 'net_common.h', 'glibc_math.h', 'glibc_math_tables.h']
 
 
 def _hipcc():
@@ -62,6 +65,27 @@ def source_hash():
     with open(os.path.join(INCLUDE, 'mtaz.h'), 'rb') as f:
         h.update(b'include/mtaz.h\0' + f.read())
     h.update(repr((SOURCES, ARCH)).encode())
+    return h.hexdigest()
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def _tu_key(src, cmd):
+    """sha256 of one translation unit's inputs: its source, every header under csrc/, include/mtaz.h
+    and the compile command."""
+    h = hashlib.sha256(repr(cmd).encode())
+    names = [src] + sorted(n for n in os.listdir(CSRC) if n.endswith('.h'))
+    for name in names:
+        with open(os.path.join(CSRC, name), 'rb') as f:
+            h.update(name.encode() + b'\0' + f.read())
+    with open(os.path.join(INCLUDE, 'mtaz.h'), 'rb') as f:
+        h.update(f.read())
     return h.hexdigest()
 
 
@@ -96,17 +120,25 @@ def build(force=False, verbose=True, diag=False):
             flags = [f for f in flags if f != 'DIAG_ONLY']
         obj = os.path.join(bdir, src + '.o')
         cmd = [hipcc, '-x', 'hip', '-std=c++17', f'--offload-arch={ARCH}', '-fPIC', '-c',
-               os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function',
-               f'-DMTAZ_SRC_SHA256="{sha}"'] + flags
+               os.path.join(CSRC, src), '-o', obj, f'-I{INCLUDE}', '-Wall', '-Wno-unused-function'] + flags
+        if src == 'mtaz_host.cpp':   # mtaz_version() carries the whole tree's hash
+            cmd.append(f'-DMTAZ_SRC_SHA256="{sha}"')
         if diag:
             cmd.append('-DMTAZ_NET_DIAG')
+        objs.append(obj)
+        # an object is reused when its source, every header of csrc/ and include/mtaz.h, and its
+        # compile command are unchanged (the network TUs take minutes)
+        key = _tu_key(src, cmd)
+        if not force and os.path.exists(obj) and _read(obj + '.key') == key:
+            continue
         if verbose:
             print(' '.join(cmd), flush=True)
-        procs.append((subprocess.Popen(cmd), cmd))
-        objs.append(obj)
-    for p, cmd in procs:
+        procs.append((subprocess.Popen(cmd), cmd, obj, key))
+    for p, cmd, obj, key in procs:
         if p.wait() != 0:
             raise RuntimeError('hipcc failed: ' + ' '.join(cmd))
+        with open(obj + '.key', 'w') as f:
+            f.write(key)
     tmp = out + '.tmp'
     cmd = [hipcc, '-shared', f'--offload-arch={ARCH}', '-o', tmp] + objs + ['-lpthread']
     if verbose:

@@ -86,6 +86,10 @@ struct Games {
   Pos* hist;              // [G*HMAX] game positions before each move (repetition)
   int32_t* nhist;
   int DMAX, HMAX;
+  // numpy legacy RandomState per game on the device (mtaz_rng.hip): the MT19937 block of game g at
+  // mt_key[g*624 .. +624] and the index of its next word (numpy's state.pos)
+  uint32_t* mt_key;
+  int32_t* mt_pos;
 };
 
 struct Leaves {
@@ -138,6 +142,8 @@ struct Params {
   // process_observation(fen) alone) and per-board deterministic, so the tables, and every result,
   // are those without the memo.  Off when the two agents search with different networks (arena).
   int memo;
+  double alpha;           // Dirichlet concentration of the root noise (exp/agent.py:82: 0.6)
+  int tau;                // fullmove number from which moves are argmax picks (exp/agent.py:113)
 };
 
 struct Dev {
@@ -220,6 +226,11 @@ constexpr int ERR_F16 = 512;   // activation exceeded the f16 range in the fp16x
 // depend on the boards sharing the workgroup.  An error only where a leaf memo would hand such a
 // result to another batch (check_err(h, true) with memo >= 1); evaluate paths clear it.
 constexpr int ERR_ZRANGE = 1024;
+// k_choose: a randint rejection loop outran the 64 words reserved for it (probability < 2^-64)
+constexpr int ERR_RNG = 2048;
+// k_select: the PUCT argmax found no child (cannot happen: a NaN score counts as the maximum, as in
+// numpy's argmax); the simulation stops instead of following an edge past the node's k
+constexpr int ERR_PUCT = 4096;
 
 struct NetBuffers {
   float* x0;              // [B][256][32]
@@ -280,6 +291,14 @@ void launch_memo_clear(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);
 void launch_gather_leaf_codes(const Dev& d, uint16_t* codes_out, int32_t* k_out, hipStream_t s);
+// device legacy RNG (mtaz_rng.hip): seed every game's MT19937 with seed_base + g; this move's
+// Dirichlet draws (Games::noise_off / noise_js layout); the action choice from the root rows of
+// k_move_end into actions[g]; the test entry of mtaz_rng_dirichlet_device
+void launch_rng_seed(const Dev& d, uint64_t seed_base, hipStream_t s);
+void launch_noise(const Dev& d, hipStream_t s);
+void launch_choose(const Dev& d, const uint16_t* codes, const uint32_t* visits, int kout, int32_t* actions, hipStream_t s);
+void launch_rng_dirichlet_test(const uint32_t* seeds, const int32_t* ks, const int64_t* offs, int n_streams, int n_vec,
+                               double alpha, double* out, double* tail, uint32_t* scratch, hipStream_t s);
 
 // net modes
 enum NetMode { NET_LEAVES = 0, NET_FULL_LOGITS = 1 };

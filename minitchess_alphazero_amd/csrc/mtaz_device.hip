@@ -718,7 +718,8 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
         const float cp = D.pr.cpuct_f * Pf;
         tt = (double)(cp * (float)sq);            // numpy 1.x: stays float32
       }
-      const double u = Q + tt / (1.0 + N);
+      double u = Q + tt / (1.0 + N);
+      u = u != u ? __builtin_inf() : u;   // numpy's argmax takes the first NaN as the maximum
       if (u > best_u) { best_u = u; best_i = c; best_cc = code; best_ch = child; }
     }
     // wave argmax of (u, first index) by DPP steps (quad permutes, half-row and row mirrors, row
@@ -727,6 +728,10 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
     // six steps).  The order (u descending, index ascending) is total, so every reduction tree
     // gives the butterfly's winner.
     const int a = wave_argmax_dpp(best_u, best_i);
+    if ((unsigned)a >= (unsigned)k) {   // (no child compared above: never with the NaN rule; no edge read past k)
+      if (lane == 0) atomicOr(D.pr.err, ERR_PUCT);
+      return;
+    }
     best_cc = (uint32_t)__builtin_amdgcn_readlane((int)best_cc, a & 63);
     best_ch = (uint32_t)__builtin_amdgcn_readlane((int)best_ch, a & 63);
     if (depth >= D.gm.DMAX) {

@@ -468,7 +468,8 @@ struct GameRec {
 enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
-  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_CHOICE_MS, ST_GAP_MS, ST_EXTRA_WAVES, ST_COUNT
+  ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_CHOICE_MS, ST_GAP_MS, ST_EXTRA_WAVES,
+  ST_RNG_DEVICE, ST_RNG_DEV_MS, ST_COUNT
 };
 
 // Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
@@ -685,6 +686,12 @@ struct mtaz_engine {
   int defer = 1;
   int ncu = 0;
   int32_t* d_remaining = nullptr;
+  // mtaz_play's numpy-legacy RNG (mtaz_set_rng_device): 1 (the default) = per-game MT19937 state in
+  // HBM, Dirichlet draws (k_noise) and action choice (k_choose) on the device; 0 = the host C++ RNG
+  // (h->rng), drawn in chunks that overlap the simulations.  The device path needs dir_alpha < 1
+  // (the reference's 0.6: every gamma attempt then takes 4 words); other alphas use the host
+  int rng_device = 1;
+  hipEvent_t rng_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // [noise begin, end, choose begin, end]
 
   ~mtaz_engine() {
     group_pool.reset();
@@ -692,6 +699,8 @@ struct mtaz_engine {
     for (mtaz_engine* p : parts) delete p;
     if (device >= 0) (void)hipSetDevice(device);
     if (noise_host) (void)hipHostFree(noise_host);
+    for (auto e : rng_ev)
+      if (e) (void)hipEventDestroy(e);
     if (pin_block) (void)hipHostFree(pin_block);
     if (err_host) (void)hipHostFree(err_host);
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -809,6 +818,8 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&gm.simc, G));
   ECHK(h->dalloc(&gm.hist, (size_t)G * gm.HMAX));
   ECHK(h->dalloc(&gm.nhist, G));
+  ECHK(h->dalloc(&gm.mt_key, (size_t)G * 624));
+  ECHK(h->dalloc(&gm.mt_pos, G));
   HIPCHK(hipMemset(gm.active, 0, G));
   HIPCHK(hipMemset(gm.agent, 0, G * 4));
   HIPCHK(hipMemset(gm.nhist, 0, G * 4));
@@ -858,6 +869,8 @@ static int engine_alloc(mtaz_engine* h) {
   pr.sqrt_tab = h->d_sqrt;
   pr.sqrt_n = sqn;
   pr.memo = h->memo;
+  pr.alpha = h->alpha;
+  pr.tau = h->tau;
   // network activations: [G][256][32] x 3
   h->nb.B = G;
   ECHK(h->dalloc(&h->nb.x0, (size_t)G * 8192));
@@ -935,6 +948,8 @@ static int check_err(mtaz_engine* h, bool memo_path = true) {
     if (e & ERR_HIST) m += " history-capacity";
     if (e & ERR_HASH) m += " hash-full";
     if (e & ERR_F16) m += " activation-exceeds-f16-range";
+    if (e & ERR_RNG) m += " rng-words";
+    if (e & ERR_PUCT) m += " puct-argmax";
     if (e & ERR_ZRANGE)
       m += " f16f8-range-with-memo (k_net_z keeps one exponent per workgroup: past 2^14 its results depend"
            " on the batch, so memo >= 1 would hand them to other games; use f16x3 or mtaz_set_memo(0))";
@@ -1498,6 +1513,61 @@ extern "C" int mtaz_set_defer(mtaz_engine* h, int mode) {
   return 0;
 }
 
+extern "C" int mtaz_set_rng_device(mtaz_engine* h, int on) {
+  if (on != 0 && on != 1) return set_err(MTAZ_E_FAIL, "rng_device must be 0 (host) or 1 (device)");
+  h->rng_device = on;
+  for (mtaz_engine* p : h->parts) p->rng_device = on;
+  return 0;
+}
+
+// the device RNG's test entry (tests/test_gpu_rng.py): stream s = RandomState(seeds[s]) draws n_vec
+// Dirichlet(alpha x ks[s]) vectors (rows of ks[s] doubles, streams one after another in out) with the
+// kernels' own code (wave_dirichlet), then one random_sample() into tail[s].  Host buffers.
+extern "C" int mtaz_rng_dirichlet_device(int device, const uint32_t* seeds, const int32_t* ks, int n_streams, int n_vec,
+                                         double alpha, double* out, double* tail) {
+  if (n_streams <= 0 || n_vec < 0) return set_err(MTAZ_E_FAIL, "n_streams must be positive, n_vec >= 0");
+  if (!(alpha > 0 && alpha < 1)) return set_err(MTAZ_E_FAIL, "the device gamma sampler needs 0 < alpha < 1");
+  std::vector<int64_t> offs(n_streams);
+  int64_t tot = 0;
+  for (int s = 0; s < n_streams; ++s) {
+    if (ks[s] <= 0 || ks[s] > KMAX) return set_err(MTAZ_E_CAPACITY, "k = %d out of [1, %d]", ks[s], KMAX);
+    offs[s] = tot;
+    tot += (int64_t)ks[s] * n_vec;
+  }
+  HIPCHK(hipSetDevice(device));
+  uint32_t *d_seeds = nullptr, *d_scr = nullptr;
+  int32_t* d_ks = nullptr;
+  int64_t* d_offs = nullptr;
+  double *d_out = nullptr, *d_tail = nullptr;
+  int rc = 0;
+  auto fin = [&](int r) {
+    (void)hipFree(d_seeds); (void)hipFree(d_scr); (void)hipFree(d_ks);
+    (void)hipFree(d_offs); (void)hipFree(d_out); (void)hipFree(d_tail);
+    return r;
+  };
+#define RNGCHK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) return fin(set_err(MTAZ_E_DEVICE, "%s", hipGetErrorString(e_))); \
+  } while (0)
+  RNGCHK(hipMalloc(&d_seeds, n_streams * 4));
+  RNGCHK(hipMalloc(&d_scr, (size_t)n_streams * 624 * 4));
+  RNGCHK(hipMalloc(&d_ks, n_streams * 4));
+  RNGCHK(hipMalloc(&d_offs, n_streams * 8));
+  RNGCHK(hipMalloc(&d_out, std::max<int64_t>(tot, 1) * 8));
+  RNGCHK(hipMalloc(&d_tail, n_streams * 8));
+  RNGCHK(hipMemcpy(d_seeds, seeds, n_streams * 4, hipMemcpyHostToDevice));
+  RNGCHK(hipMemcpy(d_ks, ks, n_streams * 4, hipMemcpyHostToDevice));
+  RNGCHK(hipMemcpy(d_offs, offs.data(), n_streams * 8, hipMemcpyHostToDevice));
+  launch_rng_dirichlet_test(d_seeds, d_ks, d_offs, n_streams, n_vec, alpha, d_out, d_tail, d_scr, nullptr);
+  RNGCHK(hipGetLastError());
+  RNGCHK(hipDeviceSynchronize());
+  if (tot) RNGCHK(hipMemcpy(out, d_out, tot * 8, hipMemcpyDeviceToHost));
+  RNGCHK(hipMemcpy(tail, d_tail, n_streams * 8, hipMemcpyDeviceToHost));
+#undef RNGCHK
+  return fin(rc);
+}
+
 extern "C" int mtaz_set_sync_mode(mtaz_engine* h, int mode) {
   if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "sync mode must be 0 (stream sync) or 1 (blocking event)");
   h->sync_mode = mode;
@@ -1913,6 +1983,7 @@ static int play_groups(mtaz_engine* h) {
     p->host_threads = std::max(1, h->host_threads / ng);   // the groups share this engine's threads
     p->sync_mode = h->sync_mode;
     p->defer = h->defer;
+    p->rng_device = h->rng_device;
     p->memo = h->memo;
     ECHK(ensure_batch_memo(p));
     sync_memo(p);
@@ -1939,7 +2010,7 @@ static int play_groups(mtaz_engine* h) {
     for (int gi = 0; gi < Gp; ++gi) std::swap(h->rec[(size_t)pi * Gp + gi], p->rec[gi]);
     h->final_outcome.insert(h->final_outcome.end(), p->final_outcome.begin(), p->final_outcome.end());
     for (int i = 0; i < ST_COUNT; ++i) {
-      if (i == ST_MAX_NODES || i == ST_MAX_EDGES || i == ST_NET_PREC || i == ST_MOVES)
+      if (i == ST_MAX_NODES || i == ST_MAX_EDGES || i == ST_NET_PREC || i == ST_MOVES || i == ST_RNG_DEVICE)
         h->stats[i] = std::max(h->stats[i], p->stats[i]);
       else if (i != ST_WALL_MS) h->stats[i] += p->stats[i];
     }
@@ -2011,7 +2082,16 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     ECHK(mtaz_set_games(h, roots.data(), nullptr, act.data(), G));
   }
   ECHK(mtaz_clear_trees(h, nullptr, 0));
-  for (int g = 0; g < G; ++g) mt_seed(h->rng[g], (uint32_t)(h->seed_base + (uint64_t)g));
+  const bool dev_rng = h->rng_device && h->alpha < 1.0;
+  if (dev_rng) {
+    launch_rng_seed(h->d, h->seed_base, h->stream);
+    HIPCHK(hipGetLastError());
+    if (h->timing)
+      for (auto& e : h->rng_ev)
+        if (!e) HIPCHK(hipEventCreate(&e));
+  } else {
+    for (int g = 0; g < G; ++g) mt_seed(h->rng[g], (uint32_t)(h->seed_base + (uint64_t)g));
+  }
   h->rec.resize(G);
   for (auto& r : h->rec) r.clear();
   h->final_outcome.assign(G, 0);
@@ -2030,7 +2110,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   uint32_t* visits = PP.visits;
   for (int g = 0; g < G; ++g) actions[g] = 0;
   ECHK(mtaz_get_games(h, roots, agents, active, outcome_v));
-  double rng_ms = 0, sync_ms = 0, choice_ms = 0, gap_ms = 0;
+  double rng_ms = 0, sync_ms = 0, choice_ms = 0, gap_ms = 0, rng_dev_ms = 0;
   double t_gap = -1;   // when the last move's root visit counts reached the host
   int moves = 0;
   for (;;) {
@@ -2062,7 +2142,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     }
     const size_t need = (size_t)std::max<int64_t>(K, 1) * h->sims;
     ECHK(ensure_noise(h, need));   // (mtaz_move_begin synchronised the stream)
-    if (need > h->noise_host_cap) {
+    if (!dev_rng && need > h->noise_host_cap) {
       // grown geometrically, as the device buffer: pinning a fresh buffer costs ~4 ms, and the
       // legal counts grow over a game's first moves (round 5a regrew it on about twenty of them)
       const size_t cap = std::max(need, 2 * h->noise_host_cap);
@@ -2075,6 +2155,13 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (int g = 0; g < G; ++g) js[g] = (int32_t)K;
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_off, offs, G * 8, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->d.gm.noise_js, js, G * 4, hipMemcpyHostToDevice, h->stream));
+    if (dev_rng) {
+      // every game's draws of the move in one launch, in stream order, ahead of its simulations
+      if (h->timing) HIPCHK(hipEventRecord(h->rng_ev[0], h->stream));
+      launch_noise(h->d, h->stream);
+      HIPCHK(hipGetLastError());
+      if (h->timing) HIPCHK(hipEventRecord(h->rng_ev[1], h->stream));
+    }
     // chunks [0, 1), [1, 3), [3, 7), [7, 15), [15, 23), ...: the GPU starts after one draw per game,
     // and each later chunk is drawn while the previous chunk's simulations run.  The chunks double
     // up to 8 draws so that a chunk's draws never take longer than the simulations they overlap:
@@ -2084,6 +2171,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     auto chunk_end = [&](int j0) { return std::min(j0 + std::min(NCH, j0 + 1), h->sims); };
     auto draw_chunk = [&](int j0) {   // draws [j0, chunk_end(j0)) of every active game
       const int je = chunk_end(j0);
+      if (dev_rng) return 0;
       parallel_for(G, h->host_threads, [&](int g) {
         if (!active[g]) return;
         const int k = root_k[g], jn = std::min(je, h->sims - root_new[g]);
@@ -2132,12 +2220,32 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     for (int g = 0; g < G; ++g)
       if (active[g]) kmx = std::max(kmx, root_k[g]);
     ts = now_ms();
-    ECHK(mtaz_move_end(h, codes, visits, nullptr, kmx));
+    if (dev_rng) {
+      // action choice on the device from the root rows k_move_end leaves in HBM; the rows and the
+      // actions then come to the host (records) with the move's one sync
+      launch_move_end(h->d, h->d_root_codes, h->d_root_visits, kmx, h->stream);
+      if (h->timing) HIPCHK(hipEventRecord(h->rng_ev[2], h->stream));
+      launch_choose(h->d, h->d_root_codes, h->d_root_visits, kmx, h->d_actions, h->stream);
+      if (h->timing) HIPCHK(hipEventRecord(h->rng_ev[3], h->stream));
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(codes, h->d_root_codes, (size_t)G * kmx * 2, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipMemcpyAsync(visits, h->d_root_visits, (size_t)G * kmx * 4, hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipMemcpyAsync(actions, h->d_actions, G * 4, hipMemcpyDeviceToHost, h->stream));
+      ECHK(check_err(h));
+      if (h->timing) {
+        float a = 0, b = 0;
+        HIPCHK(hipEventElapsedTime(&a, h->rng_ev[0], h->rng_ev[1]));
+        HIPCHK(hipEventElapsedTime(&b, h->rng_ev[2], h->rng_ev[3]));
+        rng_dev_ms += a + b;
+      }
+    } else {
+      ECHK(mtaz_move_end(h, codes, visits, nullptr, kmx));
+    }
     sync_ms += now_ms() - ts;
     t_gap = now_ms();
     // action selection (exp/agent.py:110-119)
     tr = now_ms();
-    parallel_for(G, h->host_threads, [&](int g) {
+    if (!dev_rng) parallel_for(G, h->host_threads, [&](int g) {
       if (!active[g]) return;
       const int k = root_k[g];
       const uint16_t* c = codes + (size_t)g * kmx;
@@ -2166,7 +2274,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
     // this move's records (exp/callbacks.py:40-47) from this move's buffers
     ts = now_ms();
     const int nxt = cur ^ 1;
-    HIPCHK(hipMemcpyAsync(h->d_actions, actions, G * 4, hipMemcpyHostToDevice, h->stream));
+    if (!dev_rng) HIPCHK(hipMemcpyAsync(h->d_actions, actions, G * 4, hipMemcpyHostToDevice, h->stream));
     launch_apply(h->d, h->d_actions, h->stream);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(PP.roots[nxt], h->d.gm.root, (size_t)G * sizeof(Pos), hipMemcpyDeviceToHost, h->stream));
@@ -2251,6 +2359,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_CHOICE_MS] = choice_ms;
   h->stats[ST_GAP_MS] = gap_ms;
   h->stats[ST_COMPACT_MS] = compact_ms;
+  h->stats[ST_RNG_DEVICE] = dev_rng ? 1 : 0;
+  h->stats[ST_RNG_DEV_MS] = rng_dev_ms;
   return 0;
 }
 

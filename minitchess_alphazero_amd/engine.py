@@ -25,7 +25,7 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
               'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap',
-              'memo_batch_hits', 'choice_ms', 'gap_ms', 'extra_waves']
+              'memo_batch_hits', 'choice_ms', 'gap_ms', 'extra_waves', 'rng_device', 'rng_dev_ms']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
@@ -172,6 +172,12 @@ class Engine:
         identical in every mode."""
         _lib.check(self.L.mtaz_set_defer(self.h, int(mode)))
 
+    def set_rng_device(self, on=1):
+        """Where play() runs numpy's legacy RNG (the root Dirichlet noise of exp/agent.py:82 and the
+        action choice of :114-118): 1 (default) = on the device (per-game MT19937 state in HBM, one
+        k_noise and one k_choose launch per move), 0 = on the host.  Games are identical."""
+        _lib.check(self.L.mtaz_set_rng_device(self.h, int(on)))
+
     def wave_log(self, max_waves=1 << 17):
         """Per-wave log of the last play(): int32 [waves, 3] = (leaves evaluated, game-memo hits,
         batch-memo hits)."""
@@ -222,11 +228,12 @@ class Engine:
         return {'plies': plies, 'pos': pos[:P], 'action': action[:P], 'k': k[:P], 'codes': codes[:E],
                 'visits': visits[:E], 'reward': reward[:P], 'outcome': outcome}
 
-    def episodes(self):
-        """InfoRecorder records (exp/callbacks.py:40-54), one list of dicts per game."""
+    def episodes(self, n_games=None):
+        """InfoRecorder records (exp/callbacks.py:40-54), one list of dicts per game (the first
+        n_games games only, if given)."""
         r = self.records()
         out, p, e = [], 0, 0
-        for g in range(len(r['plies'])):
+        for g in range(len(r['plies']) if n_games is None else min(int(n_games), len(r['plies']))):
             ep = []
             for _ in range(int(r['plies'][g])):
                 k = int(r['k'][p])

@@ -39,10 +39,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def rescale(sd, k):
-    """stress4's state_dict -> the reparametrised one (new tensors; exact powers of two)."""
+def rescale(sd, k, gain=None):
+    """stress4's state_dict -> the reparametrised one (new tensors; exact powers of two).  With
+    `gain` (tools/make_stress6.py) the factor is that float instead of 2^k: the same maps, no longer
+    exact in floating point (each scaled tensor is rounded once), so the result is a new net."""
     from minitchess_alphazero_amd.network import Network
-    c = float(2 ** k)
+    c = float(2 ** k) if gain is None else float(gain)
     net = Network()
     net.load_state_dict(sd)
     with torch.no_grad():
