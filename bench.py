@@ -84,8 +84,10 @@ def host_cores():
         pass
     usable = len(aff) if quota is None else max(1, min(len(aff), int(quota)))
     span = f'{aff[0]}-{aff[-1]}' if aff and aff[-1] - aff[0] + 1 == len(aff) else ','.join(map(str, aff))
+    from minitchess_alphazero_amd.launch import gpu_numa_nodes, numa_cpus
     return {'os_cpu_count': n_os, 'affinity_count': len(aff), 'affinity': span, 'cgroup_quota_cpus': quota,
-            'usable': usable}
+            'usable': usable, 'gpu_numa_nodes': gpu_numa_nodes(),
+            'numa_nodes': {str(k): len(v) for k, v in sorted(numa_cpus().items())}}
 
 
 def one_thread_jobs(gpu_sims, extra_sims=()):
@@ -126,18 +128,20 @@ def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budg
     (the value), the other sims on all cores, then the 1-thread legs (all at once).  Skipped legs
     are named in budget['skipped'], never silently dropped."""
     import multiprocessing as mp
-    seeds = [0, 1, 2] if plan == 'full' else [0]
+    # all-core legs: 2 seeded games each at the GPU's sims, the repo default 36 and C1's 32 (VERDICT r5
+    # #6: all three inside the driver's budget); the 1-thread legs (run during the warm-up) keep 3
+    seeds = [0, 1] if plan == 'full' else [0]
     others = sorted({32, *extra_sims} - {gpu_sims}, reverse=True) if plan == 'full' else sorted(set(extra_sims) - {gpu_sims})
     sims_list = sorted({gpu_sims, *others})
     ctx = mp.get_context('spawn')
     runs = {}
     skipped = budget['skipped'] if budget is not None else []
 
-    def record(sims, label, thr, games):
+    def record(sims, label, thr, games, sds=None):
         secs = [g['seconds'] for g in games]
         log(f'cpu baseline {sims} sims, {thr} thread(s): {[round(x, 1) for x in secs]} s per game')
         runs[f'{sims}sims/{label}'] = {
-            'threads': thr, 'seeds': seeds, 'seconds_per_game': [round(x, 3) for x in secs],
+            'threads': thr, 'seeds': sds or seeds, 'seconds_per_game': [round(x, 3) for x in secs],
             'games_per_s': len(secs) / sum(secs), 'plies': [g['plies'] for g in games],
             'nn_evals': [g['nn_evals'] for g in games],
             'sims_per_s': sum(g['plies'] for g in games) * sims / sum(secs)}
@@ -165,16 +169,17 @@ def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budg
     if plan == 'full' and one_thread is not None:
         # measured during the warm-up steps (start_one_thread_legs)
         for sm in one_thread['sims_list']:
-            record(sm, '1thread', 1, one_thread['games'][sm])
+            record(sm, '1thread', 1, one_thread['games'][sm], one_thread['seeds'])
     elif plan == 'full':
         # 1 thread: every (sims, seed) game at once, one single-threaded process each (each game alone
         # on its core; measured at ~2.4x the all-core seconds per game)
         if fits('1-thread legs', per_sim * max(sims_list) * 2.6 * 1.2 + 8):
-            jobs = [(sm, sd, 1) for sm in sims_list for sd in seeds]
+            seeds1 = [0, 1, 2]
+            jobs = [(sm, sd, 1) for sm in sims_list for sd in seeds1]
             with ctx.Pool(len(jobs)) as pool:
                 out = pool.map(_cpu_game, jobs, chunksize=1)
             for i, sm in enumerate(sims_list):
-                record(sm, '1thread', 1, out[i * len(seeds):(i + 1) * len(seeds)])
+                record(sm, '1thread', 1, out[i * len(seeds1):(i + 1) * len(seeds1)], seeds1)
     head = runs[f'{gpu_sims}sims/all']
     sample = (f'{len(seeds)} seeded games (np.random.seed 0..{len(seeds) - 1}) from STARTING_FEN at '
               f'{gpu_sims} sims/move on {all_threads} threads: the oracle restatement of app/puppet '
@@ -187,6 +192,42 @@ def cpu_baseline(plan, all_threads, gpu_sims, extra_sims=(), deadline=None, budg
                    f'{one_thread["gpu_host_threads"]} meanwhile), never during the timed region')
     return {'value': head['games_per_s'], 'unit': 'games/s', 'cores': all_threads, 'kind': 'port',
             'sample': sample, 'sims_per_s': head['sims_per_s'], 'runs': runs}
+
+
+# the reference's own self-play games a benched engine's games 0.. must reproduce (seeds 0..n-1 =
+# np.random.seed(g) games, seed-0 net or the C3 checkpoint): sims -> (fixture, key, weights)
+PARITY_FIXTURES = {
+    (64, None): ('trees_r2.json', 'net_seed0_64'),     # tests/golden/make_golden_r2.py
+    (36, None): ('trees_r6.json', 'net_seed0_36'),     # tests/golden/make_golden_r6.py
+    (32, None): ('trees.json', 'net_seed0'),           # tests/golden/make_golden.py
+    (256, 'c3'): ('c3.json', 'c3_256'),                # BASELINE config 3 (make_golden_r2.py)
+}
+
+
+def parity_stamp(engine, sims, weights_kind, seed_base):
+    """After a timed play (untimed): the engine's games 0.. against the reference's games of the same
+    seeds, ply for ply (observation, legal list, pi, action, reward); a plain JSON compare.  None
+    when no fixture covers this workload."""
+    fx = PARITY_FIXTURES.get((sims, weights_kind))
+    if fx is None or seed_base != 0:
+        return None
+    games = json.load(open(os.path.join(HERE, 'tests', 'golden', fx[0])))[fx[1]]
+    if engine.G < len(games):
+        return None
+    got = engine.episodes(len(games))
+    ident = plies = 0
+    first = None
+    for g, ref in enumerate(games):
+        assert ref['seed'] == g
+        plies += max(len(ref['moves']), len(got[g]))
+        for i, (a, b) in enumerate(zip(got[g], ref['moves'])):
+            if (a['observation'] == b['observation'] and a['legal_moves'] == b['legal_moves'] and a['pi'] == b['pi']
+                    and a['action'] == b['action'] and a['reward'] == b['reward']):
+                ident += 1
+            elif first is None:
+                first = {'game': g, 'ply': i}
+    return {'fixture': f'tests/golden/{fx[0]}:{fx[1]}', 'games': [g['seed'] for g in games], 'identical_plies': ident,
+            'plies': plies, 'first_mismatch': first, 'ok': ident == plies}
 
 
 def kernel_roofline(tot, prec):
@@ -302,6 +343,7 @@ def main():
 
     rank = int(os.environ.get('RANK', 0))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    node_mask = sorted(os.sched_getaffinity(0))   # before this rank pins itself to its slice
     # this rank's disjoint slice of the host cores and its host-thread budget (launch.rank_host_share)
     from minitchess_alphazero_amd.launch import pin_rank, rank_host_share
     rank_share = None
@@ -319,10 +361,20 @@ def main():
     # the CPU baseline's 1-thread legs run during setup and warm-up (rank 0 of a 1-GPU run), started
     # before this process touches the GPU
     legs = None
+    legs_mask = None
     if (world == 1 and not args.no_cpu_baseline and args.cpu_plan == 'full' and args.one_thread_during_warmup
             and rank_share is None):
         extra = (args.default_sims,) if args.default_sims and args.default_sims != args.sims else ()
         legs = start_one_thread_legs(args.sims, extra)
+        # while the legs run, this process (its main thread, the HIP runtime's threads and the engine's
+        # host threads, all started after this point) stays on the reserved cores the legs skip, so
+        # that it does not slow the legs it is compared with
+        legs_mask = sorted(os.sched_getaffinity(0))
+        leg_cores = legs[2]['cores']
+        reserved = [c for c in legs_mask if c not in set(leg_cores)][:2] if None not in leg_cores else []
+        if reserved:
+            os.sched_setaffinity(0, reserved)
+            legs[2]['gpu_process_cores'] = reserved
     import numpy as np
     import torch
     torch.set_num_threads(host_threads)
@@ -352,6 +404,7 @@ def main():
     seed_base, _ = shard(rank, world, G)
     eng = Engine(n_games=G, sims=sims, device=device, seed_base=seed_base)
     weights_sha = None
+    weights_kind = None if not args.weights else 'other'   # None: the seed-0 random init
     if args.weights:
         import hashlib
         if args.weights.endswith('.safetensors'):
@@ -366,6 +419,11 @@ def main():
             h.update(k.encode())
             h.update(v.detach().cpu().contiguous().numpy().tobytes())
         weights_sha = h.hexdigest()
+        try:
+            if weights_sha == json.load(open(os.path.join(HERE, 'tests', 'golden', 'c3.json')))['state_dict_sha256']:
+                weights_kind = 'c3'
+        except (OSError, KeyError, ValueError):
+            pass
     else:
         torch.manual_seed(0)                      # random-init weights of the reference architecture
         net_for_engine = Network()
@@ -407,11 +465,12 @@ def main():
         out = res.get()
         pool.close()
         pool.join()
+        os.sched_setaffinity(0, legs_mask)   # (threads started from here on get the whole mask)
         eng.set_host_threads(eng_threads)
         waited = elapsed() - t_wait
         per = len(meta['seeds'])
         one_thread = {**meta, 'games': {sm: out[i * per:(i + 1) * per] for i, sm in enumerate(meta['sims_list'])},
-                      'gpu_host_threads': LEG_HOST_THREADS,
+                      'gpu_host_threads': LEG_HOST_THREADS, 'gpu_process_cores': meta.get('gpu_process_cores'),
                       'overlap': (f'{args.warmup} warm-up step(s); started at {meta["t_start"]:.1f} s, the timed '
                                   f'region waited {waited:.1f} s more for them')}
         budget['one_thread_legs_wait_s'] = round(waited, 1)
@@ -435,7 +494,8 @@ def main():
             dist.barrier()
 
     KEYS = ('sims', 'nn_evals', 'memo_hits', 'memo_batch_hits', 'plies', 'trunk_ms', 'trunk_boards', 'waves', 'terminal_sims',
-            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms', 'choice_ms', 'gap_ms', 'extra_waves', 'moves')
+            'decisive', 'host_rng_ms', 'sync_ms', 'select_ms', 'compact_ms', 'choice_ms', 'gap_ms', 'extra_waves', 'moves',
+            'rng_dev_ms', 'rng_device')
 
     import resource
 
@@ -482,6 +542,10 @@ def main():
     dt, tot, prec = timed(eng, args.steps, 'main')
     games = G * args.steps * world
     step_s = dt / args.steps
+    # untimed: the last timed play's games 0.. against the reference's games of the same seeds
+    parity = parity_stamp(eng, sims, weights_kind, seed_base) if rank == 0 else None
+    if parity is not None:
+        log(f'parity vs {parity["fixture"]}: {parity["identical_plies"]}/{parity["plies"]} plies identical')
 
     def fits(label, est_s):
         """True when an optional leg of ~est_s seconds ends inside the budget (same answer on every
@@ -518,13 +582,17 @@ def main():
             others = (args.default_sims + 32) if args.cpu_plan == 'full' else args.default_sims
             cpu_rest = n_seeds * 0.35 * (sims + 1.25 * others) * 16 / max(1, host_cores()['usable']) + 15
         step36 = step_s * args.default_sims / sims * 1.15
-        n36 = 2 if agree_max(elapsed() + 2 * step36 + 5 + cpu_rest) <= args.time_budget else 1
-        if n36 == 1:
-            budget['skipped'].append({'leg': f'second {args.default_sims}-sims step', 'estimate_s': round(step36, 1)})
+        n36 = 3
+        while n36 > 1 and agree_max(elapsed() + n36 * step36 + 5 + cpu_rest) > args.time_budget:
+            n36 -= 1
+        if n36 < 3:
+            budget['skipped'].append({'leg': f'{args.default_sims}-sims steps {n36 + 1}..3', 'estimate_s': round(step36, 1)})
         dt3, tot3, prec3 = timed(eng36, n36, f'{args.default_sims} sims')
         at_default = {'sims_per_move': args.default_sims, 'value': G * world * n36 / dt3, 'unit': 'games/s', 'steps': n36,
                       'ms_per_step': dt3 * 1e3 / n36, 'roofline': kernel_roofline(tot3, prec3),
                       **counters(tot3, dt3, G * world * n36)}
+        if rank == 0:
+            at_default['parity'] = parity_stamp(eng36, args.default_sims, weights_kind, seed_base)
         eng36.close()
 
     # secondary line (opt-in, --secondary): one more timed step on the other fused network (k_net_z,
@@ -539,6 +607,24 @@ def main():
         eng.set_precision(args.precision)
         secondary = {'precision': PRECISION_NOTE[prec2], 'value': G * world / dt2, 'unit': 'games/s', 'steps': 1,
                      'ms_per_step': dt2 * 1e3, 'roofline': kernel_roofline(tot2, prec2), **counters(tot2, dt2, G * world)}
+    # N > 1: rank 0 runs the CPU baseline after the timed region on the node's usable
+    # cores while the other ranks wait idle at a barrier
+    cb_multi = None
+    if world > 1 and not args.no_cpu_baseline:
+        if rank == 0:
+            mask = sorted(os.sched_getaffinity(0))
+            os.sched_setaffinity(0, node_mask)   # the spawned games get the node's cores, not rank 0's slice
+            try:
+                hc = host_cores()
+                extra = (args.default_sims,) if args.default_sims and args.default_sims != sims else ()
+                cb_multi = cpu_baseline('quick', args.cpu_threads or hc['usable'], sims, extra,
+                                        deadline=args.time_budget, budget=budget)
+                if cb_multi is not None:
+                    cb_multi['sample'] += (f'; run by rank 0 after the timed region while the other {world - 1} '
+                                           f'rank(s) waited idle')
+            finally:
+                os.sched_setaffinity(0, mask)
+        dist.barrier()
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -606,6 +692,10 @@ def main():
                           # k_select launch; its time is outside the k_select roofline
                           'leaf_compact_avg_ms': tot['compact_ms'] / tot['waves'] if tot['waves'] else None},
         'host_threads': eng_threads,
+        # numpy's legacy RNG (Dirichlet root noise, action choice): on the device (k_noise, k_choose;
+        # rng_device_s = their kernel time over the timed steps, summed over ranks) or on the host
+        'rng_device': bool(tot['rng_device']),
+        'rng_device_s': tot['rng_dev_ms'] / 1e3,
         'host_rng_s': tot['host_rng_ms'] / 1e3,
         'host_sync_s': tot['sync_ms'] / 1e3,
         # host time between two moves' simulations (the GPU idles): action choice + records
@@ -620,6 +710,8 @@ def main():
         'defer': args.defer,
         'mtaz_src_sha256': lib_hash,
     }
+    if parity is not None:
+        line['parity'] = parity
     if rank_share is not None:
         line['rank_share'] = rank_share
     if secondary is not None:
@@ -640,11 +732,18 @@ def main():
                 at_default['cpu_baseline_games_per_s'] = r36['games_per_s']
                 at_default['cpu_baseline_sims_per_s'] = r36['sims_per_s']
                 at_default['vs_cpu_baseline'] = at_default['value'] / r36['games_per_s']
+    if cb_multi is not None:
+        line['cpu_baseline'] = cb_multi
+        line['vs_cpu_baseline'] = line['value'] / cb_multi['value']
     budget['end_s'] = round(elapsed(), 1)
     line['budget'] = budget
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    bad = [p for p in (parity, (at_default or {}).get('parity')) if p is not None and not p['ok']]
+    if bad:
+        log(f'PARITY MISMATCH: {bad}')
+        sys.exit(5)
 
 
 if __name__ == '__main__':

@@ -68,26 +68,96 @@ def cgroup_cpu_quota():
         return None
 
 
-def rank_host_share(local_rank, local_world, cores=None, quota=None):
-    """This rank's slice of the host: the ranks on a node split the process's affinity mask into
-    disjoint contiguous core ranges, and its usable CPUs (the smaller of the mask and the cgroup
-    quota) into equal thread budgets, so N ranks of host work (Dirichlet draws, action choice,
-    torch) do not oversubscribe the cores the node grants.  -> (cores, threads); cores is None
-    when the mask has fewer cores than ranks (no pinning then)."""
+def _cpulist(text):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]"""
+    out = []
+    for part in text.strip().split(','):
+        if part:
+            lo, _, hi = part.partition('-')
+            out += range(int(lo), int(hi or lo) + 1)
+    return out
+
+
+def numa_cpus(root='/sys/devices/system/node'):
+    """NUMA node -> its CPUs ({} when the kernel exposes no NUMA topology)."""
+    out = {}
+    try:
+        for name in os.listdir(root):
+            if name.startswith('node') and name[4:].isdigit():
+                with open(os.path.join(root, name, 'cpulist')) as f:
+                    out[int(name[4:])] = _cpulist(f.read())
+    except OSError:
+        return {}
+    return out
+
+
+def gpu_numa_nodes(kfd='/sys/class/kfd/kfd/topology/nodes', pci='/sys/bus/pci/devices'):
+    """HIP device index -> the NUMA node of its PCI function (-1 unknown), [] when unavailable.  The
+    KFD topology lists the GPU nodes (simd_count > 0) in the order of the HSA agents HIP enumerates;
+    each node's location_id is its PCI bus << 8 | devfn.  ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES
+    of plain indices select and reorder them as the runtime does."""
+    gpus = []
+    try:
+        for n in sorted((x for x in os.listdir(kfd) if x.isdigit()), key=int):
+            props = {}
+            with open(os.path.join(kfd, n, 'properties')) as f:
+                for line in f:
+                    kv = line.split()
+                    if len(kv) == 2:
+                        props[kv[0]] = kv[1]
+            if int(props.get('simd_count', 0)) == 0:
+                continue
+            loc, dom = int(props.get('location_id', 0)), int(props.get('domain', 0))
+            bdf = f'{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}'
+            try:
+                with open(os.path.join(pci, bdf, 'numa_node')) as f:
+                    gpus.append(int(f.read()))
+            except (OSError, ValueError):
+                gpus.append(-1)
+    except OSError:
+        return []
+    for var in ('ROCR_VISIBLE_DEVICES', 'HIP_VISIBLE_DEVICES'):
+        sel = os.environ.get(var)
+        if sel:
+            try:
+                gpus = [gpus[int(i)] for i in sel.split(',')]
+            except (ValueError, IndexError):
+                return []
+    return gpus
+
+
+def rank_host_share(local_rank, local_world, cores=None, quota=None, gpu_numa=None, node_cpus=None):
+    """This rank's slice of the host: its usable CPUs (the smaller of the mask and the cgroup quota)
+    split into equal thread budgets, so N ranks of host work (torch, the engine's host threads) do
+    not oversubscribe the cores the node grants, and a disjoint range of the affinity mask to pin to.
+    With the NUMA topology known (gpu_numa[d] = NUMA node of HIP device d, the rank's device being
+    its local rank; node_cpus[node] = that node's CPUs), the range comes from the mask's cores on its
+    GPU's NUMA node, split among the ranks whose GPUs sit on that node; otherwise
+    the whole mask is split by rank index.  -> (cores, threads); cores is None when there are fewer
+    cores than ranks to share them (no pinning then)."""
     if cores is None:
         cores = sorted(os.sched_getaffinity(0))
     if quota is None:
         quota = cgroup_cpu_quota()
     usable = len(cores) if quota is None else max(1, min(len(cores), int(quota)))
     threads = max(1, usable // max(1, local_world))
+    if gpu_numa and node_cpus and len(gpu_numa) >= local_world and gpu_numa[local_rank] in node_cpus:
+        node = gpu_numa[local_rank]
+        local = sorted(set(cores) & set(node_cpus[node]))
+        peers = [r for r in range(local_world) if gpu_numa[r] == node]
+        per = len(local) // len(peers)
+        if per >= 1:
+            i = peers.index(local_rank)
+            return local[i * per:(i + 1) * per], threads
     per = len(cores) // max(1, local_world)
     mine = cores[local_rank * per:(local_rank + 1) * per] if per >= 1 else None
     return mine, threads
 
 
 def pin_rank(local_rank, local_world):
-    """Apply rank_host_share to this process (before it starts threads); returns the thread budget."""
-    mine, threads = rank_host_share(local_rank, local_world)
+    """Apply rank_host_share to this process (before it starts threads), with the node's NUMA
+    topology when the kernel exposes it; returns the thread budget."""
+    mine, threads = rank_host_share(local_rank, local_world, gpu_numa=gpu_numa_nodes(), node_cpus=numa_cpus())
     if mine and local_world > 1:
         os.sched_setaffinity(0, mine)
     return threads

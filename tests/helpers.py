@@ -139,7 +139,16 @@ def stress_network(name='stress'):
     from oracle.net import state_dict_sha256
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
     net = Network()
-    net.load_state_dict(load_file(os.path.join(here, name, f'{name}.safetensors')))
+    if name == 'stress6':
+        # stress6 (round 6, tools/make_stress6.py, pinned by make_golden_r6.py): stress4 with its trunk in
+        # 181x larger units, a non-power-of-two gain (new significands), rebuilt from the committed
+        # stress4 and checked against its pinned sha256 below
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(here), '..', 'tools'))
+        from make_stress6 import stress6_state_dict
+        net.load_state_dict(stress6_state_dict())
+    else:
+        net.load_state_dict(load_file(os.path.join(here, name, f'{name}.safetensors')))
     meta = json.load(open(os.path.join(here, f'{name}.json')))
     assert state_dict_sha256(net) == meta['state_dict_sha256'], f'{name} checkpoint does not match its pinned sha256'
     return net.eval()

@@ -108,7 +108,8 @@ def _net(kind):
     """seed0: torch.manual_seed(0); Network().  stress: the round-3 stress checkpoint (trunk
     activations in the thousands; its k_net_y stored-units exponents leave 0 on a few positions).
     stress5: stress4 with its trunk in 2^7 larger units (exponents 1-4 on every position and 18 of
-    the 19 trunk layers, a value head whose outputs vary; tests/golden/make_golden_r5.py)."""
+    the 19 trunk layers, a value head whose outputs vary; tests/golden/make_golden_r5.py).  stress6:
+    the same with a gain of 181 (new significands, exponents 2-5; tests/golden/make_golden_r6.py)."""
     import torch
     from minitchess_alphazero_amd.network import Network
     from helpers import stress_network
@@ -118,7 +119,7 @@ def _net(kind):
     return stress_network(kind)
 
 
-@pytest.mark.parametrize('kind', ['seed0', 'stress', 'stress5'])
+@pytest.mark.parametrize('kind', ['seed0', 'stress', 'stress5', 'stress6'])
 def test_leaf_memo_leaves_games_unchanged(kind):
     """The leaf memo changes which leaves the network evaluates, not the games: with the GPU network,
     the per-game memo, the per-game + batch memo and no memo give identical records, and computed +
@@ -232,7 +233,7 @@ def test_cpp_driver_equals_python_driver():
         assert [r['reward'] for r in a] == [r['reward'] for r in b]
 
 
-@pytest.mark.parametrize('kind', ['seed0', 'stress', 'stress5'])
+@pytest.mark.parametrize('kind', ['seed0', 'stress', 'stress5', 'stress6'])
 def test_games_independent_of_batch_composition(kind):
     """Per-game results depend only on the game's seed (the multi-GPU sharding contract), also on a
     trained net whose stored-units exponents leave 0: 40 games in one engine (up to
@@ -272,7 +273,8 @@ def test_pipelined_groups_equal_single_stream():
         assert st['games'] == 8 and st['sims'] == one.stats()['sims']
 
 
-@pytest.mark.parametrize('kind,memo,mode', [('seed0', 2, 2), ('seed0', 0, 2), ('seed0', 2, 1), ('stress5', 2, 2)])
+@pytest.mark.parametrize('kind,memo,mode', [('seed0', 2, 2), ('seed0', 0, 2), ('seed0', 2, 1), ('stress5', 2, 2),
+                                            ('stress6', 2, 1)])
 def test_deferred_tails_leave_games_unchanged(kind, memo, mode):
     """Deferred tails (mtaz_set_defer, the play() default): a wave evaluates only whole rounds of
     4 boards x CUs of its leaves and the rest wait, their games selecting again only after that

@@ -209,7 +209,7 @@ def test_y_tap_skip_bit_identical():
 
 @pytest.mark.parametrize('precision,net_kind', [('f16f8', 'seed0'), ('f16f8', 'tiny'), ('f16x3', 'seed0'),
                                                ('f16x3', 'tiny'), ('f16x3', 'wide'), ('f16x3', 'stress'),
-                                               ('f16x3', 'stress5')])
+                                               ('f16x3', 'stress5'), ('f16x3', 'stress6')])
 def test_tail_launches_bit_identical(net_kind, precision):
     """The tail-balanced board assignment (k_net_z, k_net_y: the boards beyond the full rounds of
     4 x CUs go to workgroups of 1, 2 or 3 boards) computes every board exactly as 4 boards per
@@ -227,7 +227,8 @@ def test_tail_launches_bit_identical(net_kind, precision):
     import torch
     torch.manual_seed(0)
     net = {'seed0': Network, 'wide': _wide_range_net, 'tiny': _tiny_activation_net,
-           'stress': _stress_net, 'stress5': lambda: _stress_net('stress5')}[net_kind]()
+           'stress': _stress_net, 'stress5': lambda: _stress_net('stress5'),
+           'stress6': lambda: _stress_net('stress6')}[net_kind]()
     fens = random_fens(400, seed=29)
     eng = Engine(n_games=4096, sims=4)
     eng.set_precision(precision)
@@ -304,27 +305,27 @@ def _wide_range_net(gain=6.0):
 @pytest.mark.parametrize('precision,var', [('f16x3', 0), ('f16f8', 0), ('f16f8', 8192)])
 def test_dynamic_range_beyond_f16(precision, var):
     """k_net_y and k_net_z keep fp32's range (a power-of-two image scale chosen from a weight bound:
-    per board in k_net_y, per workgroup in k_net_z).  With trunk activations ~7e6 the logits match torch's fp32 eval forward to 1e-5 of
-    each row's largest logit (the fp32 error scale at these magnitudes), values (saturated tanh)
-    to 1e-5, and the best legal move agrees wherever its margin exceeds that error scale."""
-    import torch
+    per board in k_net_y, per workgroup in k_net_z).  With trunk activations ~7e6 the logits match the
+    REFERENCE's own fp32 eval forward (exp/policy.py Network on the build container's CPU,
+    tests/golden/wide_net.npz by make_golden_r6.py; VERDICT r5 #2: not torch-ROCm) to 1e-5 of each
+    row's largest logit (the fp32 error scale at these magnitudes), values (saturated tanh) to 1e-5,
+    and the best legal move agrees wherever its margin exceeds that error scale."""
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen, pos_legal
-    from minitchess_alphazero_amd.learner import collate_fn
+    from oracle.net import state_dict_sha256
     from tests_positions import random_fens
     net = _wide_range_net()
-    fens = random_fens(129, seed=9)
+    z = np.load(os.path.join(GOLDEN, 'wide_net.npz'))
+    assert state_dict_sha256(net) == str(z['state_dict_sha256'])
+    fens = [str(f) for f in z['fens']]
+    assert fens == random_fens(129, seed=9)
     eng = Engine(n_games=64, sims=4)
     eng.set_precision(precision)
     eng.set_net_variant(var)
     eng.set_weights(net)
     pos = np.stack([pos_from_fen(f) for f in fens])
     logits, values = eng.evaluate(pos)
-    rows = [{'observation': f, 'legal_moves': [], 'pi': [], 'reward': 0.0} for f in fens]
-    _, tok, clk, _ = collate_fn(rows)
-    with torch.no_grad():
-        p, v = net.cuda()((tok.cuda(), clk.cuda()))
-    p, v = p.double().cpu().numpy(), v[:, 0].double().cpu().numpy()
+    p, v = z['logits'].astype(np.float64), z['values'].astype(np.float64)
     assert np.abs(p).max() > 1e5                          # the trunk really left f16's range
     scale = np.abs(p).max(axis=1, keepdims=True)
     # k_net_z's e4m3 cross terms carry ~2^-15 of each layer's output; through this net's 9
@@ -345,12 +346,15 @@ def _stress_net(name='stress'):
     exponents 1-4 on every board, values that vary; tests/golden/make_golden_r5.py)."""
     from safetensors.torch import load_file
     from minitchess_alphazero_amd.network import Network
+    if name == 'stress6':   # rebuilt from stress4 and sha-checked (tools/make_stress6.py)
+        from helpers import stress_network
+        return stress_network('stress6')
     net = Network()
     net.load_state_dict(load_file(os.path.join(GOLDEN, name, f'{name}.safetensors')))
     return net.eval()
 
 
-@pytest.mark.parametrize('net_kind', ['wide', 'stress', 'stress5'])
+@pytest.mark.parametrize('net_kind', ['wide', 'stress', 'stress5', 'stress6'])
 def test_board_results_independent_of_batch(net_kind):
     """a board's logits and value do not depend on the other boards of its batch or
     workgroup (the reference evaluates every leaf batch-1, exp/agent.py:67-69), also once the
@@ -360,7 +364,8 @@ def test_board_results_independent_of_batch(net_kind):
     from minitchess_alphazero_amd.engine import Engine
     from minitchess_alphazero_amd.environment import pos_from_fen
     from tests_positions import random_fens
-    net = {'wide': _wide_range_net, 'stress': _stress_net, 'stress5': lambda: _stress_net('stress5')}[net_kind]()
+    net = {'wide': _wide_range_net, 'stress': _stress_net, 'stress5': lambda: _stress_net('stress5'),
+           'stress6': lambda: _stress_net('stress6')}[net_kind]()
     fens = random_fens(1300, seed=41)
     pos = np.stack([pos_from_fen(f) for f in fens])
     eng = Engine(n_games=4096, sims=4)

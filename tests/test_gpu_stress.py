@@ -40,7 +40,7 @@ TOL = 1e-5
 EXACT = ['f16x3', 'fp32']          # the precisions whose north_star claim covers this net
 
 
-CKPTS = ['stress', 'stress4', 'stress5']
+CKPTS = ['stress', 'stress4', 'stress5', 'stress6']
 
 
 def _fixture(name='stress'):
@@ -110,8 +110,29 @@ def test_stress5_checkpoint_pinned_exponents_and_values():
     assert any(r['lr'] == 0.2 for r in runs) and all(r['value_dead_from_update'] is not None for r in runs)
 
 
-def test_stress5_kernel_exponents_equal_the_emulation():
-    """The exponents k_net_y itself picks on stress5 (the stamp-instrumented build's per-board
+def test_stress6_checkpoint_pinned_exponents_and_values():
+    """stress6 (tools/make_stress6.py: stress4's trunk in 181x larger units, a
+    non-power-of-two gain) is a net with new significands (its reference outputs are not stress4's)
+    that drives k_net_y's exponents to >= 2 on every fixture position, with live values."""
+    meta = load_golden('stress6')
+    stress_network('stress6')
+    _, ref_l, ref_v = _fixture('stress6')
+    ex = meta['k_net_y_exponents']
+    assert ex['boards_any_xs_pos'] == ex['boards'] == meta['positions'] and ex['layers_xs_pos'] >= 18
+    assert ex['min_over_boards_of_max_exponent'] >= 1 and ex['xs_max'] >= 4
+    assert ref_v.std() >= 0.05 and ref_v.max() - ref_v.min() >= 0.4
+    assert meta['derivation']['gain'] == 181.0
+    # not a power-of-two copy: on the positions both fixtures hold, the reference's outputs differ
+    f4, l4, _ = _fixture('stress4')
+    f6 = _fixture('stress6')[0]
+    common = [(f6.index(f), i) for i, f in enumerate(f4) if f in f6]
+    assert len(common) >= 100
+    assert sum(not np.array_equal(ref_l[j], l4[i]) for j, i in common) >= 0.9 * len(common)
+
+
+@pytest.mark.parametrize('name', ['stress5', 'stress6'])
+def test_stress5_kernel_exponents_equal_the_emulation(name):
+    """The exponents k_net_y itself picks on stress5 / stress6 (the stamp-instrumented build's per-board
     records, Engine.net_exponents) equal tools/net_range.py's recomputation of the kernel's bound
     from a float64 forward, board by board and layer by layer: the fixtures below really run the
     nonzero-exponent path (and stress4's run none of it)."""
@@ -121,7 +142,7 @@ def test_stress5_kernel_exponents_equal_the_emulation():
     from conftest import REPO
     sys.path.insert(0, os.path.join(REPO, 'tools'))
     from net_range import fens_profile
-    for name in ('stress5', 'stress4'):
+    for name in (name, 'stress4'):
         fens = _fixture(name)[0]
         eng = Engine(n_games=64, sims=4)
         eng.set_precision('f16x3')
@@ -132,7 +153,7 @@ def test_stress5_kernel_exponents_equal_the_emulation():
         emu_mask = ((xs > 0).astype(np.int64) << np.arange(xs.shape[0])[:, None]).sum(axis=0)
         assert np.array_equal(xmax, xs.max(axis=0)), name
         assert np.array_equal(mask, emu_mask), name
-        if name == 'stress5':
+        if name != 'stress4':
             assert (xmax > 0).all()
         else:
             assert (mask == 0).all()
@@ -220,8 +241,8 @@ def test_stress_gpu_net_64_sims_vs_reference(precision):
     _l3('stress_64', precision, stress_network(), ref.eval(), [load_golden('stress')['stress_64']])
 
 
-@pytest.mark.parametrize('name', ['stress4', 'stress5'])
-@pytest.mark.parametrize('game', ['game_start', 'game_end'])
+@pytest.mark.parametrize('name,game', [('stress4', 'game_start'), ('stress4', 'game_end'), ('stress5', 'game_start'),
+                                       ('stress5', 'game_end'), ('stress6', 'game_start')])
 def test_stress4_host_leaves_64_sims_equal_reference(game, name):
     """L1 on stress4 and stress5: the reference's 64-sim games (from STARTING_FEN, and one from an
     endgame start: decisive for stress4), leaves evaluated batch-1 on the host exactly as
@@ -240,7 +261,7 @@ def test_stress4_host_leaves_64_sims_equal_reference(game, name):
     assert [x['reward'] for x in recs[0]] == [x['reward'] for x in gm['moves']]
 
 
-@pytest.mark.parametrize('name', ['stress4', 'stress5'])
+@pytest.mark.parametrize('name', ['stress4', 'stress5', 'stress6'])
 def test_stress4_gpu_net_64_sims_vs_reference(name):
     """L3 on stress4 and stress5 with the default network (k_net_y), the game from STARTING_FEN
     (on stress5 with the exponents off 0 on every layer but the stem)."""

@@ -130,7 +130,7 @@ def test_terminal_revisit_quirk(golden):
         assert seen_quirk
 
 
-@pytest.mark.parametrize('name', ['stress', 'stress4', 'stress5'])
+@pytest.mark.parametrize('name', ['stress', 'stress4', 'stress5', 'stress6'])
 def test_trained_checkpoint_outputs(name):
     """The oracle's network (exp/policy.py restated) on the trained checkpoints reproduces the
     reference's own outputs (make_golden_r3.py / make_golden_r4.py) on fixture positions: the
@@ -141,7 +141,13 @@ def test_trained_checkpoint_outputs(name):
     from safetensors.torch import load_file
     from conftest import GOLDEN, load_golden
     n = net.Network()
-    n.load_state_dict(load_file(os.path.join(GOLDEN, name, f'{name}.safetensors')))
+    if name == 'stress6':   # not committed: rebuilt from stress4 (tools/make_stress6.py), sha-pinned
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), '..', 'tools'))
+        from make_stress6 import stress6_state_dict
+        n.load_state_dict(stress6_state_dict())
+    else:
+        n.load_state_dict(load_file(os.path.join(GOLDEN, name, f'{name}.safetensors')))
     n.eval()
     assert net.state_dict_sha256(n) == load_golden(name)['state_dict_sha256']
     z = np.load(os.path.join(GOLDEN, f'{name}_net.npz'))
@@ -219,3 +225,19 @@ def test_long_list_positions_exceed_a_wave():
         assert rules.Board(f).result() == '*', f
         distinct.append(len(set(legal)) < len(legal))
     assert sum(distinct) >= 2
+
+
+def test_oracle_reproduces_the_36_sim_reference_games():
+    """The oracle's self-play (the app/puppet path restated) reproduces the reference's 36-sim seed-0
+    games of make_golden_r6.py (the repo's default sims, app/base.py:25), seed 0 ply for ply."""
+    from conftest import load_golden
+    from oracle import selfplay
+    from oracle.mcts import TorchNetEvaluator
+    games = load_golden('trees_r6')['net_seed0_36']
+    ev = TorchNetEvaluator(net.seed0_network())
+    got = selfplay.play_games(ev, 1, 36, seed_base=0)[0]
+    ref = games[0]['moves']
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert (a['observation'], list(a['legal_moves']), list(a['pi']), a['action'], a['reward']) == \
+            (b['observation'], b['legal_moves'], b['pi'], b['action'], b['reward'])
