@@ -174,6 +174,17 @@ int mtaz_set_defer(mtaz_engine* h, int mode);
  * stream draw for draw, so games are identical.  The device sampler covers 0 < dir_alpha < 1 (the
  * reference's 0.6); other alphas run on the host. */
 int mtaz_set_rng_device(mtaz_engine* h, int on);
+/* mtaz_play's schedule: 0 (default) = moves in lockstep (every game's move ends in the same wave;
+ * per-move host hand-offs); 1 = free-running moves: a game whose move is complete records it,
+ * chooses its action, steps and starts its next move on the device (one k_turn launch per wave,
+ * one wavefront per game that finished a move) while the other games keep simulating; the host
+ * only reads the active-game count every 16 waves and the records at the end.  Every game runs the
+ * same simulations on the same tables, draws and network results in both, so the records are
+ * identical; on the bench workload free-running is 1.5% slower (more waves, k_turn on every wave's
+ * critical path).
+ * Free-running needs the device RNG (mtaz_set_rng_device 1, dir_alpha < 1) and one network for both
+ * agents; mtaz_play falls back to lockstep otherwise (stat 'schedule' says which ran). */
+int mtaz_set_schedule(mtaz_engine* h, int mode);
 /* per-wave log of the last mtaz_play (up to max_waves): out[3 * w + 0] leaves evaluated,
  * [+1] game-memo hits, [+2] batch-memo hits; returns the number of waves written */
 int mtaz_wave_log(mtaz_engine* h, int32_t* out, int max_waves);

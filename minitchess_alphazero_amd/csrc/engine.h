@@ -90,6 +90,21 @@ struct Games {
   // mt_key[g*624 .. +624] and the index of its next word (numpy's state.pos)
   uint32_t* mt_key;
   int32_t* mt_pos;
+  // simulations each game has started in the play (k_leaf_compact orders pending leaves by how far
+  // their game is behind the most advanced one; with free-running moves games are on different moves)
+  int32_t* stot;
+  // free-running moves (mtaz_set_schedule 1, k_turn): each game's InfoRecorder records written on the
+  // device, ply p of game g at [g * PLY + p]; its legal lists and root visit counts appended to its
+  // region [g * RC, g * RC + rec_cur[g]) (RC = PLY x KMAX)
+  int32_t* nply;
+  int32_t* rec_cur;
+  Pos* rec_pos;
+  int32_t* rec_action;
+  int32_t* rec_k;
+  uint16_t* rec_codes;
+  uint32_t* rec_visits;
+  int PLY;
+  int64_t RC;
 };
 
 struct Leaves {
@@ -290,6 +305,12 @@ void launch_backup(const Dev& d, hipStream_t s);
 void launch_memo_clear(const Dev& d, hipStream_t s);
 void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, int kout, hipStream_t s);
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s);
+// free-running moves: (start) every active game begins its move, or (!start) every game whose move is
+// complete finishes it (record, action choice, game step) and begins the next; then the active count
+void launch_turn(const Dev& d, int start, hipStream_t s);
+void launch_count_active(const Dev& d, int32_t* out, hipStream_t s);
+// the games' appended legal lists / visit counts packed game after game at off[g] (host-computed)
+void launch_rec_pack(const Dev& d, const int64_t* off, uint16_t* codes, uint32_t* visits, hipStream_t s);
 void launch_gather_leaf_codes(const Dev& d, uint16_t* codes_out, int32_t* k_out, hipStream_t s);
 // device legacy RNG (mtaz_rng.hip): seed every game's MT19937 with seed_base + g; this move's
 // Dirichlet draws (Games::noise_off / noise_js layout); the action choice from the root rows of

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "legacy_rng.h"
 
 namespace mtaz {
 
@@ -479,6 +480,7 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
   const bool act = ((reinterpret_cast<const uint32_t*>(D.gm.active)[g >> 2] >> (8 * (g & 3))) & 0xffu) != 0;
   const uint32_t pend = defer ? D.lf.gnode[g] : NONE;
   const int sc = defer ? D.gm.simc[g] : 0;
+  const int st0 = defer ? D.gm.stot[g] : 0;
   const int ag = D.gm.agent[g];
   Pos pos = D.gm.root[g];
   uint32_t n = D.gm.root_node[g];
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
   load_rules_lds(&s_rt);
   // the values are needed here, so every load above is issued before the gates branch (the
   // compiler otherwise sinks each load into the branch that uses it, one round trip after another)
-  asm volatile("" ::"v"((uint32_t)act), "v"(pend), "v"(sc), "v"(ag), "v"(pos.sq[0]), "v"(pos.sq[1]), "v"(pos.sq[2]),
+  asm volatile("" ::"v"((uint32_t)act), "v"(pend), "v"(sc), "v"(st0), "v"(ag), "v"(pos.sq[0]), "v"(pos.sq[1]), "v"(pos.sq[2]),
                "v"(pos.sq[3]), "v"(pos.info), "v"(n), "v"(noff), "v"(njs), "v"(rnew), "v"(nn2.x), "v"(nn2.y),
                "v"(ne2.x), "v"(ne2.y));
   if (!defer) {
@@ -505,7 +507,10 @@ __global__ __launch_bounds__(64) void k_select(Dev D, int sim, int defer) {
     if (lane == 0) D.lf.ghit[g] = 0;
     if (!act || pend != NONE) return;
     if (sc >= D.pr.sims) return;
-    if (lane == 0) D.gm.simc[g] = sc + 1;
+    if (lane == 0) {
+      D.gm.simc[g] = sc + 1;
+      D.gm.stot[g] = st0 + 1;
+    }
     sim = sc;
   }
 #ifdef MTAZ_NET_DIAG
@@ -799,7 +804,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
       nd[j] = in ? D.lf.gnode[g0 + j] : NONE;
       ag[j] = in ? D.gm.agent[g0 + j] : 0;
       load_pos_words(ps[j], D.lf.gpos, in ? g0 + j : -1);
-      sc[j] = in ? D.gm.simc[g0 + j] - 1 : 0;
+      sc[j] = in ? D.gm.stot[g0 + j] - 1 : 0;   // (the play's simulation count: games may be on different moves)
       const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
       hits += hk == 1;
       bhits += hk == 2;
@@ -877,7 +882,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
   if (defer) {   // pass 0: the most advanced leaf's simulation index
     int m = 0;
     for (int g = tid; g < G; g += 1024)
-      if (D.lf.gnode[g] != NONE) m = max(m, D.gm.simc[g] - 1);
+      if (D.lf.gnode[g] != NONE) m = max(m, D.gm.stot[g] - 1);
     for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
     if (lane == 0) atomicMax(&s_smax, m);
     __syncthreads();
@@ -886,7 +891,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
   const int smax = s_smax;
   auto bucket = [&](int g) {
     if (!defer) return 0;
-    const int lag = smax - (D.gm.simc[g] - 1);
+    const int lag = smax - (D.gm.stot[g] - 1);
     return NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
   };
   if (defer) {   // pass 1: leaves per bucket
@@ -1186,13 +1191,11 @@ void launch_move_end(const Dev& d, uint16_t* codes_out, uint32_t* visits_out, in
 }
 
 // Game step (exp/environment.py:68-82) + game-level result with history (fivefold
-// repetition compares the positions since the last zeroing move).
-__global__ void k_apply(Dev D, const int32_t* __restrict__ actions) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= D.pr.G || !D.gm.active[g]) return;
+// repetition compares the positions since the last zeroing move).  One thread; returns whether the
+// game goes on, with its new root in *next.
+__device__ bool game_step(const Dev& D, int g, int code, Pos* next) {
   const Pos p = D.gm.root[g];
   const BB b = unpack(p);
-  const int code = actions[g];
   bool ok = code >= 0 && code < NUM_ACTIONS;
   int from = 0, to = 0;
   if (ok) {
@@ -1207,7 +1210,7 @@ __global__ void k_apply(Dev D, const int32_t* __restrict__ actions) {
     atomicOr(D.pr.err, ok ? ERR_HIST : ERR_ILLEGAL);
     D.gm.active[g] = 0;
     D.gm.outcome[g] = -1;
-    return;
+    return false;
   }
   Pos* hist = D.gm.hist + (size_t)g * D.gm.HMAX;
   hist[nh] = p;
@@ -1223,10 +1226,158 @@ __global__ void k_apply(Dev D, const int32_t* __restrict__ actions) {
   D.gm.nhist[g] = nh + 1;
   D.gm.outcome[g] = oc;
   if (oc != ONGOING) D.gm.active[g] = 0;
+  *next = np;
+  return oc == ONGOING;
+}
+
+__global__ void k_apply(Dev D, const int32_t* __restrict__ actions) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= D.pr.G || !D.gm.active[g]) return;
+  Pos np;
+  (void)game_step(D, g, actions[g], &np);
 }
 
 void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s) {
   hipLaunchKernelGGL(k_apply, dim3((d.pr.G + 127) / 128), dim3(128), 0, s, d, actions);
+}
+
+// Free-running moves (mtaz_set_schedule 1).  A game whose move is complete (all
+// `sims` simulations started, no leaf pending: its last backup ran in the previous wave) finishes
+// it here, one wavefront per game, at the start of a wave, and its next move's first simulation
+// runs in the same wave's k_select, so no game waits for the others' moves:
+//   record (exp/callbacks.py:40-47): root position, legal list, visit counts, the action;
+//   action choice (exp/agent.py:110-119) from the root's visit counts on the game's RandomState;
+//   game step (exp/environment.py:68-82, k_apply's rules and repetition history);
+//   move start as k_move_begin (exp/agent.py:57: is the new root in the agent's table? k, new);
+//   the new move's sims - root_new Dirichlet vectors (exp/agent.py:81-82) into the game's own noise
+//   region [g * sims * KMAX, ...) with stride k.
+// The game's stream runs choice(move t) then noise(move t + 1), the reference's order.  `start`: the
+// play's first move of every active game (move start + noise only).
+__global__ __launch_bounds__(64) void k_turn(Dev D, int start) {
+#pragma clang fp contract(off)
+  __shared__ LegalLds s_l;
+  __shared__ RuleTables s_rt;
+  __shared__ uint32_t s_mt[2][rng::MT_N];
+  __shared__ double s_g[rng::GAMMA_BUF];   // the choice's pi (KMAX), then the gammas
+  __shared__ double s_inv[64];
+  __shared__ unsigned long long s_u;
+  __shared__ Pos s_root;
+  __shared__ int s_go;
+  const int g = blockIdx.x, lane = threadIdx.x;
+  if (!D.gm.active[g]) return;
+  if (!start && (D.gm.simc[g] < D.pr.sims || D.lf.gnode[g] != NONE)) return;
+  const Trees& T = D.tr;
+  rng::WaveMT mt{s_mt};
+  mt.load(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos[g], lane);
+  Pos root = D.gm.root[g];
+  int ag = D.gm.agent[g];
+  if (!start) {
+    const int t = 2 * g + ag;
+    const size_t nbase = (size_t)t * T.NC;
+    uint32_t n = D.gm.root_node[g], slot;
+    if (n >= (uint32_t)D.tr.n_nodes[t] || !pos_eq(T.node_pos[nbase + n], root)) n = tree_find(T, t, root, &slot);
+    if (n == NONE) {
+      if (lane == 0) atomicOr(D.pr.err, ERR_ROOT);
+      return;
+    }
+    const NodeHdr hd = T.node_hdr[nbase + n];
+    const int k = hdr_k(hd), p = D.gm.nply[g];
+    const uint32_t e0 = hd.e0;
+    const int64_t cur = D.gm.rec_cur[g];
+    if (k <= 0 || k > KMAX || p >= D.gm.PLY || cur + k > D.gm.RC) {
+      if (lane == 0) atomicOr(D.pr.err, k <= 0 ? ERR_ROOT : k > KMAX ? ERR_KMAX : ERR_HIST);
+      return;
+    }
+    uint16_t* rc = D.gm.rec_codes + (size_t)g * D.gm.RC + cur;
+    uint32_t* rv = D.gm.rec_visits + (size_t)g * D.gm.RC + cur;
+    for (int c = lane; c < k; c += 64) {
+      rc[c] = T.e_code[(size_t)e0 + c];
+      rv[c] = T.e_N[(size_t)e0 + c];
+    }
+    const int idx = rng::wave_choose(mt, T.e_N + e0, k, (int)(root.info >> 16), D.pr.tau, s_g, &s_u, D.pr.err, lane);
+    if (lane == 0) {
+      const int action = idx >= 0 ? (int)T.e_code[(size_t)e0 + idx] : -1;
+      const size_t r = (size_t)g * D.gm.PLY + p;
+      D.gm.rec_pos[r] = root;
+      D.gm.rec_action[r] = action;
+      D.gm.rec_k[r] = k;
+      D.gm.nply[g] = p + 1;
+      D.gm.rec_cur[g] = (int32_t)(cur + k);
+      Pos np;
+      s_go = game_step(D, g, action, &np) ? 1 : 0;
+      s_root = np;
+    }
+    __syncthreads();
+    if (!s_go) {
+      mt.store(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos + g, lane);
+      return;
+    }
+    root = s_root;   // (game_step's stores, passed to the other lanes through LDS)
+    ag ^= 1;
+  }
+  // the new move (k_move_begin): the root in the agent's table?  its legal count
+  const int t = 2 * g + ag;
+  uint32_t slot;
+  const uint32_t n = tree_find(T, t, root, &slot);
+  int k = 0, rnew = 0;
+  if (n != NONE) {
+    const NodeHdr hd = T.node_hdr[(size_t)t * T.NC + n];
+    if (hdr_term(hd) && lane == 0) atomicOr(D.pr.err, ERR_ROOT);
+    k = hdr_k(hd);
+  } else {
+    load_rules_lds(&s_rt);
+    const BB b = unpack(root);
+    __syncthreads();
+    k = wave_legal(b, D.pr.flags, s_rt, s_l);
+    rnew = 1;
+    if (k <= 0 && lane == 0) atomicOr(D.pr.err, k < 0 ? ERR_KMAX : ERR_ROOT);
+  }
+  const int64_t noff = (int64_t)g * D.pr.sims * KMAX;
+  if (lane == 0) {
+    D.gm.root_node[g] = n;
+    D.gm.root_k[g] = k;
+    D.gm.root_new[g] = rnew;
+    D.gm.simc[g] = 0;
+    D.gm.noise_off[g] = noff;
+    D.gm.noise_js[g] = k;
+  }
+  if (k > 0 && k <= KMAX && D.pr.sims - rnew > 0)
+    rng::wave_dirichlet(mt, D.pr.alpha, k, D.pr.sims - rnew, D.gm.noise + noff, k, s_g, s_inv, lane);
+  mt.store(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos + g, lane);
+}
+
+void launch_turn(const Dev& d, int start, hipStream_t s) {
+  hipLaunchKernelGGL(k_turn, dim3(d.pr.G), dim3(64), 0, s, d, start);
+}
+
+// the active games' count into *out
+__global__ __launch_bounds__(256) void k_count_active(Dev D, int32_t* __restrict__ out) {
+  int c = 0;
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < D.pr.G; g += gridDim.x * 256) c += D.gm.active[g] != 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+void launch_count_active(const Dev& d, int32_t* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, 4, s);
+  hipLaunchKernelGGL(k_count_active, dim3(16), dim3(256), 0, s, d, out);
+}
+
+// game g's appended legal lists and visit counts (rec_cur[g] entries) to codes / visits at off[g]
+__global__ __launch_bounds__(256) void k_rec_pack(Dev D, const int64_t* __restrict__ off, uint16_t* __restrict__ codes,
+                                                  uint32_t* __restrict__ visits) {
+  const int g = blockIdx.x;
+  const int n = D.gm.rec_cur[g];
+  const size_t src = (size_t)g * D.gm.RC;
+  const int64_t dst = off[g];
+  for (int i = threadIdx.x; i < n; i += 256) {
+    codes[dst + i] = D.gm.rec_codes[src + i];
+    visits[dst + i] = D.gm.rec_visits[src + i];
+  }
+}
+
+void launch_rec_pack(const Dev& d, const int64_t* off, uint16_t* codes, uint32_t* visits, hipStream_t s) {
+  hipLaunchKernelGGL(k_rec_pack, dim3(d.pr.G), dim3(256), 0, s, d, off, codes, visits);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -469,7 +469,7 @@ enum Stat {
   ST_PLIES, ST_SIMS, ST_NN_EVALS, ST_TERMINAL_SIMS, ST_TRUNK_MS, ST_TRUNK_BOARDS, ST_WAVES, ST_HOST_RNG_MS,
   ST_WALL_MS, ST_GAMES, ST_DECISIVE, ST_MOVES, ST_TRUNK_LAUNCHES, ST_MAX_NODES, ST_MAX_EDGES, ST_SYNC_MS, ST_NET_PREC, ST_SELECT_MS,
   ST_NODE_CAP, ST_EDGE_CAP, ST_COMPACT_MS, ST_MEMO_HITS, ST_POOL_EDGES, ST_POOL_CAP, ST_MEMO_BATCH_HITS, ST_CHOICE_MS, ST_GAP_MS, ST_EXTRA_WAVES,
-  ST_RNG_DEVICE, ST_RNG_DEV_MS, ST_COUNT
+  ST_RNG_DEVICE, ST_RNG_DEV_MS, ST_SCHEDULE, ST_COUNT
 };
 
 // Host worker pool for the per-move work (Dirichlet draws, action choice): one pool per calling
@@ -631,6 +631,7 @@ struct mtaz_engine {
   int32_t* d_count_log = nullptr;
   double* d_sqrt = nullptr;
   int count_log_cap = 0;
+  bool last_play_grouped = false;       // the last mtaz_play ran in pipeline groups (mtaz_wave_log)
   size_t noise_cap = 0;
   double* noise_host = nullptr;         // pinned staging of mtaz_play's draw-major noise
   size_t noise_host_cap = 0;
@@ -692,6 +693,19 @@ struct mtaz_engine {
   // (the reference's 0.6: every gamma attempt then takes 4 words); other alphas use the host
   int rng_device = 1;
   hipEvent_t rng_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // [noise begin, end, choose begin, end]
+  // mtaz_play's schedule (mtaz_set_schedule): 0 (default) = moves in lockstep (every game's move ends
+  // with the same wave, host hand-offs per move); 1 = free-running moves: a game that completes a move
+  // finishes it and starts the next on the device (k_turn) within the wave loop, so no game waits for
+  // the others' moves and the host syncs only every few waves.  Identical games; measured 1.5% slower
+  // on the bench workload, hence not the default.  Free-running needs the
+  // device RNG and one network for both agents; otherwise mtaz_play runs lockstep.
+  int schedule = 0;
+  std::vector<hipEvent_t> ev_turn;      // per free-running wave: [k_turn begin, end]
+  int32_t* cnt_host = nullptr;          // pinned: the active-game count of free-running play
+  int64_t* d_rec_off = nullptr;
+  uint16_t* d_pack_codes = nullptr;     // the packed records of a free-running play (grown)
+  uint32_t* d_pack_visits = nullptr;
+  size_t pack_cap = 0;
 
   ~mtaz_engine() {
     group_pool.reset();
@@ -701,6 +715,10 @@ struct mtaz_engine {
     if (noise_host) (void)hipHostFree(noise_host);
     for (auto e : rng_ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto e : ev_turn) (void)hipEventDestroy(e);
+    if (cnt_host) (void)hipHostFree(cnt_host);
+    if (d_pack_codes) (void)hipFree(d_pack_codes);
+    if (d_pack_visits) (void)hipFree(d_pack_visits);
     if (pin_block) (void)hipHostFree(pin_block);
     if (err_host) (void)hipHostFree(err_host);
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -806,7 +824,9 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&gm.root_node, G));
   HIPCHK(hipMemset(gm.root_node, 0xff, G * 4));
   ECHK(h->dalloc(&gm.agent, G));
-  ECHK(h->dalloc(&gm.active, G));
+  // (k_select reads the active bytes as aligned 32-bit words: the allocation is padded to whole words,
+  // the padding zeroed below with the rest)
+  ECHK(h->dalloc(&gm.active, (size_t)(G + 3) / 4 * 4));
   ECHK(h->dalloc(&gm.outcome, G));
   ECHK(h->dalloc(&gm.root_new, G));
   ECHK(h->dalloc(&gm.root_k, G));
@@ -820,7 +840,11 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&gm.nhist, G));
   ECHK(h->dalloc(&gm.mt_key, (size_t)G * 624));
   ECHK(h->dalloc(&gm.mt_pos, G));
-  HIPCHK(hipMemset(gm.active, 0, G));
+  ECHK(h->dalloc(&gm.stot, G));
+  HIPCHK(hipMemset(gm.stot, 0, (size_t)G * 4));
+  gm.PLY = gm.HMAX;   // a game has at most HMAX plies (k_apply's history capacity)
+  gm.RC = (int64_t)gm.PLY * KMAX;
+  HIPCHK(hipMemset(gm.active, 0, (size_t)(G + 3) / 4 * 4));
   HIPCHK(hipMemset(gm.agent, 0, G * 4));
   HIPCHK(hipMemset(gm.nhist, 0, G * 4));
   HIPCHK(hipMemset(gm.outcome, 0, G * 4));
@@ -844,7 +868,8 @@ static int engine_alloc(mtaz_engine* h) {
   ECHK(h->dalloc(&h->d_trees, T));
   // waves (two per simulation and move: deferred tails add waves at the end of a move); three ints
   // each (evaluated leaves, game / batch memo hits)
-  h->count_log_cap = 2 * h->sims * (2 * max_moves + 8);
+  // the deferred-tail guard of mtaz_play lets a move run sims + 4 sims + 8 waves
+  h->count_log_cap = (5 * h->sims + 8) * (2 * max_moves + 8);
   ECHK(h->dalloc(&h->d_count_log, 3 * (size_t)h->count_log_cap));
   ECHK(h->dalloc(&h->d_remaining, 1));
   HIPCHK(hipMemset(lf.gnode, 0xff, (size_t)G * 4));   // no leaf pending
@@ -1500,6 +1525,15 @@ extern "C" int mtaz_set_pipeline(mtaz_engine* h, int groups) {
 
 // per-wave log of the last mtaz_play: [waves][evaluated leaves, game-memo hits, batch-memo hits]
 extern "C" int mtaz_wave_log(mtaz_engine* h, int32_t* out, int max_waves) {
+  if (h->last_play_grouped) {   // the groups' logs, group after group
+    int n = 0;
+    for (mtaz_engine* p : h->parts) {
+      const int r = mtaz_wave_log(p, out + 3 * (size_t)n, max_waves - n);
+      if (r < 0) return r;
+      n += r;
+    }
+    return n;
+  }
   const int n = std::min(std::min(h->wave, h->count_log_cap), max_waves);
   if (n > 0) HIPCHK(hipMemcpy(out, h->d_count_log, (size_t)n * 3 * 4, hipMemcpyDeviceToHost));
   return n;
@@ -1510,6 +1544,13 @@ extern "C" int mtaz_set_defer(mtaz_engine* h, int mode) {
     return set_err(MTAZ_E_FAIL, "defer must be 0 (every leaf each wave), 1 (deferred tails) or 2 (every remainder)");
   h->defer = mode;
   for (mtaz_engine* p : h->parts) p->defer = mode;
+  return 0;
+}
+
+extern "C" int mtaz_set_schedule(mtaz_engine* h, int mode) {
+  if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "schedule must be 0 (moves in lockstep) or 1 (free-running moves)");
+  h->schedule = mode;
+  for (mtaz_engine* p : h->parts) p->schedule = mode;
   return 0;
 }
 
@@ -1984,6 +2025,7 @@ static int play_groups(mtaz_engine* h) {
     p->sync_mode = h->sync_mode;
     p->defer = h->defer;
     p->rng_device = h->rng_device;
+    p->schedule = h->schedule;
     p->memo = h->memo;
     ECHK(ensure_batch_memo(p));
     sync_memo(p);
@@ -2010,7 +2052,8 @@ static int play_groups(mtaz_engine* h) {
     for (int gi = 0; gi < Gp; ++gi) std::swap(h->rec[(size_t)pi * Gp + gi], p->rec[gi]);
     h->final_outcome.insert(h->final_outcome.end(), p->final_outcome.begin(), p->final_outcome.end());
     for (int i = 0; i < ST_COUNT; ++i) {
-      if (i == ST_MAX_NODES || i == ST_MAX_EDGES || i == ST_NET_PREC || i == ST_MOVES || i == ST_RNG_DEVICE)
+      if (i == ST_MAX_NODES || i == ST_MAX_EDGES || i == ST_NET_PREC || i == ST_MOVES || i == ST_RNG_DEVICE ||
+          i == ST_SCHEDULE)
         h->stats[i] = std::max(h->stats[i], p->stats[i]);
       else if (i != ST_WALL_MS) h->stats[i] += p->stats[i];
     }
@@ -2051,6 +2094,125 @@ static int ensure_play_pinned(mtaz_engine* h) {
   return 0;
 }
 
+// ---- free-running moves (mtaz_set_schedule 1) ------------------------------
+static int ensure_free_run(mtaz_engine* h) {
+  Games& gm = h->d.gm;
+  if (gm.rec_pos) return 0;
+  const size_t G = (size_t)h->G;
+  ECHK(h->dalloc(&gm.nply, G));
+  ECHK(h->dalloc(&gm.rec_cur, G));
+  ECHK(h->dalloc(&gm.rec_pos, G * gm.PLY));
+  ECHK(h->dalloc(&gm.rec_action, G * gm.PLY));
+  ECHK(h->dalloc(&gm.rec_k, G * gm.PLY));
+  ECHK(h->dalloc(&gm.rec_codes, G * (size_t)gm.RC));
+  ECHK(h->dalloc(&gm.rec_visits, G * (size_t)gm.RC));
+  ECHK(h->dalloc(&h->d_rec_off, G));
+  HIPCHK(hipHostMalloc(&h->cnt_host, 4, hipHostMallocDefault));
+  return 0;
+}
+
+// The play's waves with no per-move host step: each wave is k_turn (games whose move is complete
+// record it, choose, step and start the next move, noise included) + select / leaf list / network /
+// backup; the host reads the active-game count every W waves.  Every game runs the simulations of
+// each move in order on the same tables, draws and network results as in lockstep, so the records
+// are identical; only the wave each simulation runs in differs.  The records come from the device at
+// the end.  -> moves = the longest game's plies.
+static int play_free(mtaz_engine* h, int* moves, double* sync_ms, double* turn_ms) {
+  const int G = h->G;
+  Games& gm = h->d.gm;
+  ECHK(ensure_free_run(h));
+  ECHK(ensure_noise(h, (size_t)G * h->sims * KMAX));   // each game's region: sims draws x KMAX
+  HIPCHK(hipMemsetAsync(gm.nply, 0, (size_t)G * 4, h->stream));
+  HIPCHK(hipMemsetAsync(gm.rec_cur, 0, (size_t)G * 4, h->stream));
+  HIPCHK(hipMemsetAsync(gm.simc, 0, (size_t)G * 4, h->stream));
+  HIPCHK(hipMemsetAsync(h->d.lf.gnode, 0xff, (size_t)G * 4, h->stream));
+  launch_turn(h->d, 1, h->stream);
+  HIPCHK(hipGetLastError());
+  constexpr int W = 16;   // waves between the host's reads of the active count
+  for (;;) {
+    for (int i = 0; i < W; ++i) {
+      if (h->timing) {
+        const size_t need = 2 * (size_t)(h->wave + 1);
+        while (h->ev_turn.size() < need) {
+          hipEvent_t e;
+          HIPCHK(hipEventCreate(&e));
+          h->ev_turn.push_back(e);
+        }
+        HIPCHK(hipEventRecord(h->ev_turn[2 * h->wave], h->stream));
+      }
+      launch_turn(h->d, 0, h->stream);
+      if (h->timing) HIPCHK(hipEventRecord(h->ev_turn[2 * h->wave + 1], h->stream));
+      ECHK(sim_gpu(h, 0, 1, h->defer));
+    }
+    launch_count_active(h->d, h->d_remaining, h->stream);
+    HIPCHK(hipMemcpyAsync(h->cnt_host, h->d_remaining, 4, hipMemcpyDeviceToHost, h->stream));
+    const double ts = now_ms();
+    ECHK(check_err(h));   // (synchronises the stream)
+    *sync_ms += now_ms() - ts;
+    if (*h->cnt_host == 0) break;
+    if (h->wave >= h->count_log_cap)
+      return set_err(MTAZ_E_FAIL, "free-running moves: %d games still active after %d waves", *h->cnt_host, h->wave);
+  }
+  // the records: per game its plies, appended legal lists and visit counts packed game after game
+  std::vector<int32_t> nply(G), cur(G), outc(G);
+  HIPCHK(hipMemcpy(nply.data(), gm.nply, (size_t)G * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(cur.data(), gm.rec_cur, (size_t)G * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(outc.data(), gm.outcome, (size_t)G * 4, hipMemcpyDeviceToHost));
+  std::vector<int64_t> off(G + 1, 0);
+  for (int g = 0; g < G; ++g) off[g + 1] = off[g] + cur[g];
+  const size_t tot = (size_t)std::max<int64_t>(off[G], 1);
+  if (tot > h->pack_cap) {
+    if (h->d_pack_codes) HIPCHK(hipFree(h->d_pack_codes));
+    if (h->d_pack_visits) HIPCHK(hipFree(h->d_pack_visits));
+    const size_t cap = std::max(tot, 2 * h->pack_cap);
+    h->d_pack_codes = nullptr;
+    h->d_pack_visits = nullptr;
+    h->pack_cap = 0;
+    HIPCHK(hipMalloc(&h->d_pack_codes, cap * 2));
+    HIPCHK(hipMalloc(&h->d_pack_visits, cap * 4));
+    h->pack_cap = cap;
+  }
+  HIPCHK(hipMemcpy(h->d_rec_off, off.data(), (size_t)G * 8, hipMemcpyHostToDevice));
+  launch_rec_pack(h->d, h->d_rec_off, h->d_pack_codes, h->d_pack_visits, h->stream);
+  HIPCHK(hipGetLastError());
+  const size_t PLY = (size_t)gm.PLY;
+  std::vector<Pos> rpos((size_t)G * PLY);
+  std::vector<int32_t> ract((size_t)G * PLY), rk((size_t)G * PLY);
+  std::vector<uint16_t> codes(tot);
+  std::vector<uint32_t> visits(tot);
+  HIPCHK(hipMemcpyAsync(rpos.data(), gm.rec_pos, rpos.size() * sizeof(Pos), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(ract.data(), gm.rec_action, ract.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(rk.data(), gm.rec_k, rk.size() * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(codes.data(), h->d_pack_codes, tot * 2, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(visits.data(), h->d_pack_visits, tot * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(stream_wait(h));
+  parallel_for(G, h->host_threads, [&](int g) {
+    int64_t e = off[g];
+    for (int p = 0; p < nply[g]; ++p) {
+      const size_t r = (size_t)g * PLY + p;
+      h->rec[g].add(rpos[r], ract[r], codes.data() + e, visits.data() + e, rk[r]);
+      e += rk[r];
+    }
+  });
+  int mx = 0;
+  double sims = 0;
+  for (int g = 0; g < G; ++g) {
+    h->final_outcome[g] = outc[g];
+    mx = std::max(mx, nply[g]);
+    sims += (double)nply[g] * h->sims;
+  }
+  *moves = mx;
+  h->stats[ST_SIMS] = sims;
+  h->stats[ST_EXTRA_WAVES] = std::max(0.0, (double)h->wave - (double)mx * h->sims);
+  if (h->timing)
+    for (int w = 0; w < h->wave; ++w) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, h->ev_turn[2 * w], h->ev_turn[2 * w + 1]));
+      *turn_ms += ms;
+    }
+  return 0;
+}
+
 extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   if (!h->weights_ok) return set_err(MTAZ_E_FAIL, "weights not set (mtaz_set_weights)");
   if (n_games > h->G || n_games <= 0) return set_err(MTAZ_E_CAPACITY, "n_games=%d (engine has %d)", n_games, h->G);
@@ -2064,7 +2226,8 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
       }
     }
   }
-  if (h->groups > 1 && !two_nets && !from_current && n_games == h->G) return play_groups(h);
+  h->last_play_grouped = h->groups > 1 && !two_nets && !from_current && n_games == h->G;
+  if (h->last_play_grouped) return play_groups(h);
   HIPCHK(hipSetDevice(h->device));
   ECHK(ensure_batch_memo(h));   // (released while pipeline groups played)
   const double t0 = now_ms();
@@ -2097,7 +2260,13 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->final_outcome.assign(G, 0);
   h->wave = 0;
   h->n_played = n_games;
-
+  HIPCHK(hipMemsetAsync(h->d.gm.stot, 0, (size_t)G * 4, h->stream));
+  const bool free_run = dev_rng && h->schedule == 1 && !two_nets;
+  double rng_ms = 0, sync_ms = 0, choice_ms = 0, gap_ms = 0, rng_dev_ms = 0;
+  int moves = 0;
+  if (free_run) {
+    ECHK(play_free(h, &moves, &sync_ms, &rng_dev_ms));
+  } else {
   ECHK(ensure_play_pinned(h));
   auto& PP = h->pin;
   int cur = 0;   // PP.roots[cur] / PP.active[cur]: this move's game states
@@ -2110,9 +2279,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   uint32_t* visits = PP.visits;
   for (int g = 0; g < G; ++g) actions[g] = 0;
   ECHK(mtaz_get_games(h, roots, agents, active, outcome_v));
-  double rng_ms = 0, sync_ms = 0, choice_ms = 0, gap_ms = 0, rng_dev_ms = 0;
   double t_gap = -1;   // when the last move's root visit counts reached the host
-  int moves = 0;
   for (;;) {
     int n_active = 0;
     for (int g = 0; g < G; ++g) n_active += active[g];
@@ -2295,6 +2462,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   }
   if (two_nets) activate_slot(h, 0);
   for (int g = 0; g < G; ++g) h->final_outcome[g] = outcome_v[g];
+  }   // lockstep
   // stats
   const int nlog = std::min(h->wave, h->count_log_cap);
   std::vector<int32_t> clog(3 * (size_t)nlog), counts(nlog);
@@ -2361,6 +2529,7 @@ extern "C" int mtaz_play(mtaz_engine* h, int n_games, int from_current) {
   h->stats[ST_COMPACT_MS] = compact_ms;
   h->stats[ST_RNG_DEVICE] = dev_rng ? 1 : 0;
   h->stats[ST_RNG_DEV_MS] = rng_dev_ms;
+  h->stats[ST_SCHEDULE] = free_run ? 1 : 0;
   return 0;
 }
 

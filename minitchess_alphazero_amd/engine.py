@@ -25,7 +25,8 @@ from .environment import MOVE_CAP, RULES_FLAGS, STARTING_FEN, pos_from_fen, pos_
 STAT_NAMES = ['plies', 'sims', 'nn_evals', 'terminal_sims', 'trunk_ms', 'trunk_boards', 'waves', 'host_rng_ms',
               'wall_ms', 'games', 'decisive', 'moves', 'trunk_launches', 'max_nodes', 'max_edges', 'sync_ms', 'net_precision',
               'select_ms', 'node_cap', 'edge_cap', 'compact_ms', 'memo_hits', 'pool_edges', 'pool_cap',
-              'memo_batch_hits', 'choice_ms', 'gap_ms', 'extra_waves', 'rng_device', 'rng_dev_ms']
+              'memo_batch_hits', 'choice_ms', 'gap_ms', 'extra_waves', 'rng_device', 'rng_dev_ms',
+              'schedule']
 
 # algorithmic work of one leaf evaluation: 319,122,946 MAC
 FLOP_PER_EVAL = 638_245_892
@@ -177,6 +178,12 @@ class Engine:
         action choice of :114-118): 1 (default) = on the device (per-game MT19937 state in HBM, one
         k_noise and one k_choose launch per move), 0 = on the host.  Games are identical."""
         _lib.check(self.L.mtaz_set_rng_device(self.h, int(on)))
+
+    def set_schedule(self, mode=1):
+        """play()'s schedule: 0 (default) = moves in lockstep, 1 = free-running moves (a game that
+        completes a move finishes it and starts the next on the device while the others keep
+        simulating).  Games are identical; free-running needs the device RNG and one network."""
+        _lib.check(self.L.mtaz_set_schedule(self.h, int(mode)))
 
     def wave_log(self, max_waves=1 << 17):
         """Per-wave log of the last play(): int32 [waves, 3] = (leaves evaluated, game-memo hits,

@@ -273,23 +273,26 @@ def test_pipelined_groups_equal_single_stream():
         assert st['games'] == 8 and st['sims'] == one.stats()['sims']
 
 
-@pytest.mark.parametrize('kind,memo,mode', [('seed0', 2, 2), ('seed0', 0, 2), ('seed0', 2, 1), ('stress5', 2, 2),
-                                            ('stress6', 2, 1)])
-def test_deferred_tails_leave_games_unchanged(kind, memo, mode):
+@pytest.mark.parametrize('kind,memo,mode,G', [('seed0', 2, 2, 4096), ('seed0', 0, 2, 4096), ('seed0', 2, 1, 4096),
+                                              ('stress5', 2, 2, 4096), ('stress6', 2, 1, 4096),
+                                              ('seed0', 2, 1, 4096 + 700), ('seed0', 0, 2, 4096 + 700)])
+def test_deferred_tails_leave_games_unchanged(kind, memo, mode, G):
     """Deferred tails (mtaz_set_defer, the play() default): a wave evaluates only whole rounds of
     4 boards x CUs of its leaves and the rest wait, their games selecting again only after that
     leaf's backup; each move ends with the waves the lagging games need.  Every game still runs its
     simulations in order on the same tables, noise and network results, so the records equal the
     every-leaf-every-wave schedule's bit for bit, and every expansion is evaluated or supplied by
     the memo in both (the reference's count).  4096 games: the waves hold more than one round of
-    leaves, so leaves are really deferred (extra_waves > 0)."""
+    leaves, so leaves are really deferred (extra_waves > 0).  4796 games: the leaf list
+    is built in chunks of 4,096 games (k_leaf_compact's multi-chunk path with one scan per lag bucket)."""
     net = _net(kind)
     out = {}
     for defer in (0, mode):
-        eng = _engine(4096, 8, seed_base=900)
+        eng = _engine(G, 8, seed_base=900)
         eng.set_weights(net)
         eng.set_memo(memo)
         eng.set_defer(defer)
+        eng.set_schedule(0)   # moves in lockstep, the default (free-running moves: the test below)
         st = eng.play()
         out[defer] = (st, eng.records())
         eng.close()
@@ -301,3 +304,34 @@ def test_deferred_tails_leave_games_unchanged(kind, memo, mode):
     assert s0['extra_waves'] == 0 and s1['extra_waves'] > 0
     print(f"{kind} memo {memo} defer {mode}: {s1['extra_waves']:.0f} extra waves over {s1['moves']:.0f} moves; "
           f"waves {s0['waves']:.0f} -> {s1['waves']:.0f}")
+
+
+@pytest.mark.parametrize('kind,G,defer', [('seed0', 4096, 1), ('seed0', 4096, 0), ('seed0', 4096 + 700, 2),
+                                          ('stress5', 4096, 1), ('stress6', 1024, 1)])
+def test_free_running_moves_leave_games_unchanged(kind, G, defer):
+    """with free-running moves (mtaz_set_schedule 1; lockstep stays the default) a game
+    that completes a move records it, chooses, steps and starts its next move on the device (k_turn)
+    while the others keep simulating, so games drift onto different moves within one wave.  Every
+    game still runs its simulations in order on its own tables with its own RandomState draws and
+    the same network results, so every record equals the lockstep schedule's bit for bit (and the
+    reference's count of evaluations is unchanged)."""
+    net = _net(kind)
+    out = {}
+    for sched in (0, 1):
+        eng = _engine(G, 8, seed_base=300)
+        eng.set_weights(net)
+        eng.set_memo(2)
+        eng.set_defer(defer)
+        eng.set_schedule(sched)
+        st = eng.play()
+        assert st['schedule'] == sched and st['rng_device'] == 1
+        out[sched] = (st, eng.records())
+        eng.close()
+    (s0, r0), (s1, r1) = out[0], out[1]
+    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+        assert np.array_equal(r1[key], r0[key]), key
+    assert s1['nn_evals'] + s1['memo_hits'] == s0['nn_evals'] + s0['memo_hits']
+    assert s1['sims'] == s0['sims'] and s1['terminal_sims'] == s0['terminal_sims']
+    assert s1['moves'] == s0['moves'] and s1['plies'] == s0['plies']
+    print(f"{kind} G {G} defer {defer}: waves lockstep {s0['waves']:.0f} (extra {s0['extra_waves']:.0f}) -> "
+          f"free-running {s1['waves']:.0f} (extra {s1['extra_waves']:.0f})")
