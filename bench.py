@@ -578,9 +578,12 @@ def main():
         # steps if the budget allows; at the driver's --steps 20 it does not: profiles/r05/final2)
         cpu_rest = 0.0
         if world == 1 and not args.no_cpu_baseline:
-            n_seeds = 3 if args.cpu_plan == 'full' else 1
+            # the all-core legs still to come (cpu_baseline: 2 seeds each at the GPU's sims, 36 and 32 in
+            # the full plan): 0.32 s per sim per game on 16 cores (round 6: 0.317 at 64, 36 and 32 sims),
+            # plus the legs' process starts
+            n_seeds = 2 if args.cpu_plan == 'full' else 1
             others = (args.default_sims + 32) if args.cpu_plan == 'full' else args.default_sims
-            cpu_rest = n_seeds * 0.35 * (sims + 1.25 * others) * 16 / max(1, host_cores()['usable']) + 15
+            cpu_rest = n_seeds * 0.32 * (sims + others) * 16 / max(1, host_cores()['usable']) + 10
         step36 = step_s * args.default_sims / sims * 1.15
         n36 = 3
         while n36 > 1 and agree_max(elapsed() + n36 * step36 + 5 + cpu_rest) > args.time_budget:

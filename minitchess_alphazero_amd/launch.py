@@ -91,14 +91,43 @@ def numa_cpus(root='/sys/devices/system/node'):
     return out
 
 
+def _drm_numa_nodes(drm='/sys/class/drm'):
+    """Fallback without a KFD topology: the AMD display / accelerator PCI functions behind
+    /sys/class/drm/card*, in PCI address order (the order HIP enumerates them by default), with
+    their numa_node."""
+    found = {}
+    try:
+        for name in os.listdir(drm):
+            if not (name.startswith('card') and name[4:].isdigit()):
+                continue
+            dev = os.path.realpath(os.path.join(drm, name, 'device'))
+            try:
+                with open(os.path.join(dev, 'vendor')) as f:
+                    vendor = f.read().strip()
+                with open(os.path.join(dev, 'class')) as f:
+                    cls = f.read().strip()
+                with open(os.path.join(dev, 'numa_node')) as f:
+                    numa = int(f.read())
+            except (OSError, ValueError):
+                continue
+            if vendor == '0x1002' and (cls.startswith('0x03') or cls.startswith('0x12')):
+                found[os.path.basename(dev)] = numa
+    except OSError:
+        return []
+    return [found[b] for b in sorted(found)]
+
+
 def gpu_numa_nodes(kfd='/sys/class/kfd/kfd/topology/nodes', pci='/sys/bus/pci/devices'):
     """HIP device index -> the NUMA node of its PCI function (-1 unknown), [] when unavailable.  The
     KFD topology lists the GPU nodes (simd_count > 0) in the order of the HSA agents HIP enumerates;
-    each node's location_id is its PCI bus << 8 | devfn.  ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES
+    each node's location_id is its PCI bus << 8 | devfn.  Without a KFD topology, the AMD GPUs
+    behind /sys/class/drm in PCI address order.  ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES
     of plain indices select and reorder them as the runtime does."""
     gpus = []
+    if not os.path.isdir(kfd):
+        gpus = _drm_numa_nodes()
     try:
-        for n in sorted((x for x in os.listdir(kfd) if x.isdigit()), key=int):
+        for n in sorted((x for x in os.listdir(kfd) if x.isdigit()), key=int) if not gpus else []:
             props = {}
             with open(os.path.join(kfd, n, 'properties')) as f:
                 for line in f:

@@ -111,3 +111,22 @@ def test_topology_readers_parse_sysfs(tmp_path):
         assert gpu_numa_nodes(str(kfd), str(pci)) == [0]
     finally:
         del os.environ['HIP_VISIBLE_DEVICES']
+
+
+def test_drm_fallback_orders_gpus_by_pci_address(tmp_path):
+    """Without a KFD topology the AMD GPUs behind /sys/class/drm/card* count, in PCI address order."""
+    from minitchess_alphazero_amd.launch import _drm_numa_nodes
+    drm, pci = tmp_path / 'drm', tmp_path / 'pci'
+    devs = {'0000:c1:00.0': ('0x1002', '0x120000', 1), '0000:05:00.0': ('0x1002', '0x038000', 0),
+            '0000:07:00.0': ('0x8086', '0x030000', 0)}
+    for bdf, (vendor, cls, numa) in devs.items():
+        d = pci / bdf
+        d.mkdir(parents=True)
+        (d / 'vendor').write_text(vendor + '\n')
+        (d / 'class').write_text(cls + '\n')
+        (d / 'numa_node').write_text(f'{numa}\n')
+    for i, bdf in enumerate(['0000:c1:00.0', '0000:05:00.0', '0000:07:00.0']):
+        (drm / f'card{i}').mkdir(parents=True)
+        os.symlink(pci / bdf, drm / f'card{i}' / 'device')
+    (drm / 'renderD128').mkdir()
+    assert _drm_numa_nodes(str(drm)) == [0, 1]
