@@ -20,6 +20,8 @@ def main():
     ap.add_argument('--games', type=int, default=4096)
     ap.add_argument('--sims', type=int, default=64)
     ap.add_argument('--lib', default=None, help='library path (default: build the diagnostic one)')
+    ap.add_argument('--select-ahead', type=int, default=None,
+                    help='Engine.set_select_ahead: only with a library built with profiles/r06/select_ahead/select_ahead.diff')
     args = ap.parse_args()
     if args.lib:
         os.environ['MTAZ_LIB'] = args.lib
@@ -38,6 +40,8 @@ def main():
     eng = Engine(n_games=args.games, sims=args.sims)
     eng.set_weights(Network())
     eng.set_timing(True)
+    if args.select_ahead is not None:
+        eng.set_select_ahead(args.select_ahead)
     out = (ctypes.c_ulonglong * 8)()
     assert f(out, 1) == 0
     st = eng.play()
@@ -45,7 +49,7 @@ def main():
     v = np.array(list(out), dtype=np.float64)
     waves = max(v[0], 1.0)
     names = ['waves', 'find', 'select', 'legal', 'outcome', 'insert_init_backup', 'total', 'depth']
-    res = {'games': args.games, 'sims': args.sims, 'waves': int(v[0]),
+    res = {'games': args.games, 'sims': args.sims, 'select_ahead': args.select_ahead, 'waves': int(v[0]),
            'cycles_per_wave': {n: v[i] / waves for i, n in enumerate(names) if 0 < i < 7},
            'mean_depth': v[7] / waves,
            'select_ms_total': st['select_ms'], 'sims_total': st['sims'], 'plies': st['plies'],
