@@ -322,11 +322,11 @@ def main():
                          'event (Engine.set_sync_mode); -1 (default) = 1 when this rank has a share of a '
                          'multi-rank node (N > 1 or --rank-share), else 0 (profiles/r05/hostshare: +2.1%% '
                          'at the 2-CPU share, neutral at 16)')
-    ap.add_argument('--defer', type=int, default=1, choices=[0, 1, 2],
-                    help='deferred tails (Engine.set_defer): 1 (default) = a wave whose remainder beyond whole '
-                         'rounds of 4 boards x CUs would take a tail launch evaluates the whole rounds and the '
-                         'rest of its leaves wait for the next wave; 2 = every remainder waits; 0 = every leaf '
-                         'every wave (round 4). Results are identical')
+    ap.add_argument('--defer', type=int, default=2, choices=[0, 1, 2],
+                    help='deferred tails (Engine.set_defer): 2 (default, round 6) = a wave evaluates its whole '
+                         'rounds of 4 boards x CUs and the rest of its leaves wait for the next wave; 1 = only a '
+                         'remainder a tail launch would take waits (round 5); 0 = every leaf every wave (round 4). '
+                         'Results are identical (profiles/r06/sched2)')
     ap.add_argument('--one-thread-during-warmup', type=int, default=1, choices=[0, 1],
                     help='1 (default): run the CPU baseline 1-thread legs during engine setup and the '
                          'untimed warm-up steps (collected before the timed region); 0: after the timed '

@@ -155,8 +155,8 @@ int mtaz_set_host_threads(mtaz_engine* h, int n);
  * so the waiting thread sleeps instead of holding a CPU (8 ranks share one node's host cores:
  * bench.py --sync-mode, --rank-share).  Results are identical in both modes. */
 int mtaz_set_sync_mode(mtaz_engine* h, int mode);
-/* Deferred tails in mtaz_play (1 = default: remainders of at most 3 boards per CU, which would take
- * a tail launch, wait; 2 = every remainder waits, partial rounds too; 0 = off).  The network runs in full rounds of 4 boards
+/* Deferred tails in mtaz_play (2 = default since round 6: every remainder waits, partial rounds too;
+ * 1 = remainders of at most 3 boards per CU, which would take a tail launch, wait; 0 = off).  The network runs in full rounds of 4 boards
  * per CU; a simulation wave whose leaf count n is not a multiple of that round (4 x CUs) used to
  * end with a tail launch whose 1-3-board workgroups stream all weights for few boards.  With
  * deferral a wave evaluates only the whole rounds; the remaining leaves stay pending and lead the
@@ -166,6 +166,13 @@ int mtaz_set_sync_mode(mtaz_engine* h, int mode);
  * draws and network results, so games, tables and records are identical in both modes; only the
  * wave each simulation runs in moves.  The fine-grained API (mtaz_sim_select ...) is unaffected. */
 int mtaz_set_defer(mtaz_engine* h, int mode);
+/* Which leaves a deferred-tail wave evaluates first (its list's order; the rest of the list waits):
+ * 0 (default, round 6) = the least advanced games first (simulations started in the play, relative to
+ * the least advanced leaf: 0, 1, 2, 3+; game order within), so the leaders wait and no game falls far
+ * behind the others, which sets how many waves a move's end needs; 1 = round 5's order (lag behind
+ * the most advanced leaf: 3+, 2, 1, 0), where one game far ahead put most leaves in the 3+ bucket
+ * and game order then chose whom to defer.  Results are identical; for the A/B. */
+int mtaz_set_lag_order(mtaz_engine* h, int order);
 /* Where mtaz_play runs numpy's legacy RNG (exp/agent.py:82 Dirichlet noise, :114-118 action choice):
  * 1 (default) = on the device: per-game MT19937 state in HBM, each move's Dirichlet draws in one
  * launch (k_noise: one wavefront per game, 64 gamma attempts at once) and the action choice in

@@ -60,6 +60,7 @@ SIGNATURES = {
     'mtaz_set_host_threads': (c_int, [c_void_p, c_int]),
     'mtaz_set_sync_mode': (c_int, [c_void_p, c_int]),
     'mtaz_set_defer': (c_int, [c_void_p, c_int]),
+    'mtaz_set_lag_order': (c_int, [c_void_p, c_int]),
     'mtaz_set_rng_device': (c_int, [c_void_p, c_int]),
     'mtaz_set_schedule': (c_int, [c_void_p, c_int]),
     'mtaz_wave_log': (c_int, [c_void_p, P_i32, c_int]),

@@ -93,6 +93,9 @@ struct Games {
   // simulations each game has started in the play (k_leaf_compact orders pending leaves by how far
   // their game is behind the most advanced one; with free-running moves games are on different moves)
   int32_t* stot;
+  // free-running moves: the Dirichlet vectors drawn so far in the game's current move (k_turn draws them
+  // in chunks as the simulations come to need them, round 6)
+  int32_t* ndraw;
   // free-running moves (mtaz_set_schedule 1, k_turn): each game's InfoRecorder records written on the
   // device, ply p of game g at [g * PLY + p]; its legal lists and root visit counts appended to its
   // region [g * RC, g * RC + rec_cur[g]) (RC = PLY x KMAX)
@@ -159,6 +162,10 @@ struct Params {
   int memo;
   double alpha;           // Dirichlet concentration of the root noise (exp/agent.py:82: 0.6)
   int tau;                // fullmove number from which moves are argmax picks (exp/agent.py:113)
+  // deferred-tail play's leaf order (k_leaf_compact; mtaz_set_lag_order): 0 (default, round 6) =
+  // by simulations ahead of the least advanced leaf, ascending (buckets 0, 1, 2, 3+); 1 = round 5's:
+  // by lag behind the most advanced leaf, descending (3+, 2, 1, 0)
+  int lag_order;
 };
 
 struct Dev {

@@ -783,11 +783,15 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
   __shared__ int s_w2[16][2];
   __shared__ int s_hits[2];
   __shared__ int s_bk[NBK];   // leaves per lag bucket (pass 1), then the bucket's next slot
-  __shared__ int s_smax;
+  __shared__ int s_smax, s_smin;
   const int G = D.pr.G, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool ahead = D.pr.lag_order == 0;   // buckets by simulations ahead of the least advanced leaf
   if (tid < 2) s_hits[tid] = 0;
   if (tid < NBK) s_bk[tid] = 0;
-  if (tid == 0) s_smax = 0;
+  if (tid == 0) {
+    s_smax = 0;
+    s_smin = 0x7fffffff;
+  }
   __syncthreads();
   if (defer && G <= 1024 * PER) {
     // deferred-tail play, one chunk (G <= 4,096): every game's leaf, agent, position and lag loaded
@@ -797,7 +801,7 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     uint32_t nd[PER];
     int ag[PER], sc[PER], bk[PER];
     uint32_t ps[PER][5];   // positions as words (an array of Pos compiles to scratch copies)
-    int hits = 0, bhits = 0, m = 0;
+    int hits = 0, bhits = 0, m = 0, mn = 0x7fffffff;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const bool in = g0 + j < G;
@@ -808,12 +812,21 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
       const int hk = in ? (int)D.lf.ghit[g0 + j] : 0;
       hits += hk == 1;
       bhits += hk == 2;
-      if (nd[j] != NONE) m = max(m, sc[j]);
+      if (nd[j] != NONE) {
+        m = max(m, sc[j]);
+        mn = min(mn, sc[j]);
+      }
     }
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-    if (lane == 0) atomicMax(&s_smax, m);
+    for (int o = 32; o > 0; o >>= 1) {
+      m = max(m, __shfl_xor(m, o, 64));
+      mn = min(mn, __shfl_xor(mn, o, 64));
+    }
+    if (lane == 0) {
+      atomicMax(&s_smax, m);
+      atomicMin(&s_smin, mn);
+    }
     __syncthreads();
-    const int smx = s_smax;
+    const int smx = s_smax, smn = s_smin;
     // the thread's leaves per bucket and its memo hits, 16-bit fields of three words (every field's
     // block total is at most G <= 4,096, so no field carries into the next): one block scan of the
     // three words places every bucket's leaves and gives the totals (round 5a: one block scan per
@@ -821,8 +834,13 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     uint32_t w01 = 0, w23 = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int lag = smx - sc[j];
-      bk[j] = NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
+      if (ahead) {
+        const int d = sc[j] - smn;
+        bk[j] = d < NBK - 1 ? (d > 0 ? d : 0) : NBK - 1;
+      } else {
+        const int lag = smx - sc[j];
+        bk[j] = NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
+      }
       if (nd[j] != NONE) {
         const uint32_t one = 1u << (16 * (bk[j] & 1));
         if (bk[j] < 2) w01 += one;
@@ -879,18 +897,32 @@ __global__ __launch_bounds__(1024) void k_leaf_compact(Dev D, int32_t* __restric
     }
     return;
   }
-  if (defer) {   // pass 0: the most advanced leaf's simulation index
-    int m = 0;
+  if (defer) {   // pass 0: the most and the least advanced leaf's simulation index
+    int m = 0, mn = 0x7fffffff;
     for (int g = tid; g < G; g += 1024)
-      if (D.lf.gnode[g] != NONE) m = max(m, D.gm.stot[g] - 1);
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-    if (lane == 0) atomicMax(&s_smax, m);
+      if (D.lf.gnode[g] != NONE) {
+        m = max(m, D.gm.stot[g] - 1);
+        mn = min(mn, D.gm.stot[g] - 1);
+      }
+    for (int o = 32; o > 0; o >>= 1) {
+      m = max(m, __shfl_xor(m, o, 64));
+      mn = min(mn, __shfl_xor(mn, o, 64));
+    }
+    if (lane == 0) {
+      atomicMax(&s_smax, m);
+      atomicMin(&s_smin, mn);
+    }
     __syncthreads();
   }
-  // lag bucket of game g's leaf, 0 = the largest lag behind the most advanced leaf (listed first)
-  const int smax = s_smax;
+  // lag bucket of game g's leaf, 0 = listed first: the least advanced leaves (round 5: the largest
+  // lag behind the most advanced leaf)
+  const int smax = s_smax, smin = s_smin;
   auto bucket = [&](int g) {
     if (!defer) return 0;
+    if (ahead) {
+      const int d = (D.gm.stot[g] - 1) - smin;
+      return d < NBK - 1 ? (d > 0 ? d : 0) : NBK - 1;
+    }
     const int lag = smax - (D.gm.stot[g] - 1);
     return NBK - 1 - (lag < NBK - 1 ? (lag > 0 ? lag : 0) : NBK - 1);
   };
@@ -1253,6 +1285,10 @@ void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s) {
 //   region [g * sims * KMAX, ...) with stride k.
 // The game's stream runs choice(move t) then noise(move t + 1), the reference's order.  `start`: the
 // play's first move of every active game (move start + noise only).
+// Dirichlet vectors per k_turn draw in free-running play: about 40 gammas, which the wave's 64
+// attempts of one round usually cover (shape 0.6 accepts ~4 in 5)
+__device__ __forceinline__ int turn_noise_chunk(int k) { return k >= 40 ? 1 : 40 / k; }
+
 __global__ __launch_bounds__(64) void k_turn(Dev D, int start) {
 #pragma clang fp contract(off)
   __shared__ LegalLds s_l;
@@ -1265,7 +1301,23 @@ __global__ __launch_bounds__(64) void k_turn(Dev D, int start) {
   __shared__ int s_go;
   const int g = blockIdx.x, lane = threadIdx.x;
   if (!D.gm.active[g]) return;
-  if (!start && (D.gm.simc[g] < D.pr.sims || D.lf.gnode[g] != NONE)) return;
+  if (!start && (D.gm.simc[g] < D.pr.sims || D.lf.gnode[g] != NONE)) {
+    // mid-move: the next chunk of the move's Dirichlet vectors once the game's next simulation needs
+    // a vector not drawn yet (simulation j takes vector j - root_new, exp/agent.py:81-82).  The
+    // vectors come in order from the game's stream, all before the move's action choice, so the
+    // stream is drawn exactly as in one launch per move; drawn in chunks, a move start no longer puts
+    // all of them on the wave's critical path (round 6: 70 us per wave for 64 vectors)
+    const int sc = D.gm.simc[g], rnew = D.gm.root_new[g], nd = D.gm.ndraw[g], k = D.gm.root_k[g];
+    const int need = D.pr.sims - rnew;
+    if (sc - rnew < nd || nd >= need || k <= 0 || k > KMAX) return;
+    const int c = min(turn_noise_chunk(k), need - nd);
+    rng::WaveMT mt{s_mt};
+    mt.load(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos[g], lane);
+    rng::wave_dirichlet(mt, D.pr.alpha, k, c, D.gm.noise + D.gm.noise_off[g] + (int64_t)nd * k, k, s_g, s_inv, lane);
+    mt.store(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos + g, lane);
+    if (lane == 0) D.gm.ndraw[g] = nd + c;
+    return;
+  }
   const Trees& T = D.tr;
   rng::WaveMT mt{s_mt};
   mt.load(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos[g], lane);
@@ -1341,8 +1393,10 @@ __global__ __launch_bounds__(64) void k_turn(Dev D, int start) {
     D.gm.noise_off[g] = noff;
     D.gm.noise_js[g] = k;
   }
-  if (k > 0 && k <= KMAX && D.pr.sims - rnew > 0)
-    rng::wave_dirichlet(mt, D.pr.alpha, k, D.pr.sims - rnew, D.gm.noise + noff, k, s_g, s_inv, lane);
+  // the move's first chunk of Dirichlet vectors (the rest as its simulations come to need them, above)
+  const int c = (k > 0 && k <= KMAX) ? min(turn_noise_chunk(k), D.pr.sims - rnew) : 0;
+  if (c > 0) rng::wave_dirichlet(mt, D.pr.alpha, k, c, D.gm.noise + noff, k, s_g, s_inv, lane);
+  if (lane == 0) D.gm.ndraw[g] = c > 0 ? c : 0;
   mt.store(D.gm.mt_key + (size_t)g * rng::MT_N, D.gm.mt_pos + g, lane);
 }
 

@@ -682,9 +682,10 @@ struct mtaz_engine {
   int sync_mode = 0;
   hipEvent_t sync_ev = nullptr;
   // deferred tails (mtaz_set_defer): in mtaz_play each wave evaluates only the whole rounds of
-  // 4 boards x ncu leaves; the rest wait for the next wave (Games::simc, k_leaf_compact).  1 (the
-  // default): the remainders a tail launch would take wait; 2: every remainder waits
-  int defer = 1;
+  // 4 boards x ncu leaves; the rest wait for the next wave (Games::simc, k_leaf_compact).  2 (the
+  // default since round 6's leaf order): every remainder waits; 1: the remainders a tail launch would
+  // take wait, a larger one runs as a partial round
+  int defer = 2;
   int ncu = 0;
   int32_t* d_remaining = nullptr;
   // mtaz_play's numpy-legacy RNG (mtaz_set_rng_device): 1 (the default) = per-game MT19937 state in
@@ -894,6 +895,7 @@ static int engine_alloc(mtaz_engine* h) {
   pr.sqrt_tab = h->d_sqrt;
   pr.sqrt_n = sqn;
   pr.memo = h->memo;
+  pr.lag_order = 0;
   pr.alpha = h->alpha;
   pr.tau = h->tau;
   // network activations: [G][256][32] x 3
@@ -1547,6 +1549,13 @@ extern "C" int mtaz_set_defer(mtaz_engine* h, int mode) {
   return 0;
 }
 
+extern "C" int mtaz_set_lag_order(mtaz_engine* h, int order) {
+  if (order != 0 && order != 1) return set_err(MTAZ_E_FAIL, "lag order must be 0 (round 6) or 1 (round 5)");
+  h->d.pr.lag_order = order;
+  for (mtaz_engine* p : h->parts) p->d.pr.lag_order = order;
+  return 0;
+}
+
 extern "C" int mtaz_set_schedule(mtaz_engine* h, int mode) {
   if (mode != 0 && mode != 1) return set_err(MTAZ_E_FAIL, "schedule must be 0 (moves in lockstep) or 1 (free-running moves)");
   h->schedule = mode;
@@ -2027,6 +2036,7 @@ static int play_groups(mtaz_engine* h) {
     p->rng_device = h->rng_device;
     p->schedule = h->schedule;
     p->memo = h->memo;
+    p->d.pr.lag_order = h->d.pr.lag_order;
     ECHK(ensure_batch_memo(p));
     sync_memo(p);
     p->seed_base = h->seed_base + (uint64_t)i * Gp;
@@ -2100,6 +2110,7 @@ static int ensure_free_run(mtaz_engine* h) {
   if (gm.rec_pos) return 0;
   const size_t G = (size_t)h->G;
   ECHK(h->dalloc(&gm.nply, G));
+  ECHK(h->dalloc(&gm.ndraw, G));
   ECHK(h->dalloc(&gm.rec_cur, G));
   ECHK(h->dalloc(&gm.rec_pos, G * gm.PLY));
   ECHK(h->dalloc(&gm.rec_action, G * gm.PLY));

@@ -161,17 +161,22 @@ class Engine:
         """Host threads of the per-move work (0 = the process's affinity mask, at most 16)."""
         _lib.check(self.L.mtaz_set_host_threads(self.h, int(n)))
 
-    def set_defer(self, mode=1):
-        """Deferred tails in play() (1, the default): a simulation wave whose leaves beyond its whole
-        rounds of 4 boards x CUs would take a tail launch (at most 3 boards per CU) evaluates only
-        the whole rounds; the rest stay pending for the next wave, whose
-        list puts them first (a game selects again only after its leaf's backup, so its
+    def set_defer(self, mode=2):
+        """Deferred tails in play() (2, the default since round 6): a simulation wave evaluates only
+        its whole rounds of 4 boards x CUs; the rest stay pending for the next wave, whose list puts
+        the least advanced games first (a game selects again only after its leaf's backup, so its
         simulations run in order, exactly as in lockstep), and each move ends with the waves its
-        lagging games still need.  0 = every leaf every wave (the round-4 schedule); 2 = every
-        remainder waits, also one the main launch would run as a partial round of 4-board
-        workgroups (profiles/r05/t11: the same wall time with 32% more waves).  Results are
-        identical in every mode."""
+        lagging games still need.  1 = only a remainder a tail launch would take (at most 3 boards
+        per CU) waits, a larger one runs as a partial round (round 5's default); 0 = every leaf every
+        wave (the round-4 schedule).  With round 6's leaf order mode 2 is 1-2% faster than mode 1
+        (profiles/r06/sched2).  Results are identical in every mode."""
         _lib.check(self.L.mtaz_set_defer(self.h, int(mode)))
+
+    def set_lag_order(self, order=0):
+        """Deferred-tail play's leaf order: 0 (default) = the least advanced games first (the
+        leaders wait), 1 = round 5's order (lag behind the most advanced leaf).  Games are identical;
+        only the waves a move needs change."""
+        _lib.check(self.L.mtaz_set_lag_order(self.h, int(order)))
 
     def set_rng_device(self, on=1):
         """Where play() runs numpy's legacy RNG (the root Dirichlet noise of exp/agent.py:82 and the

@@ -28,7 +28,7 @@ def _bench_engine(sims, rng_device=1):
     eng.set_weights(Network())
     eng.set_precision('f16x3')
     eng.set_memo(2)
-    eng.set_defer(1)
+    eng.set_defer(2)
     eng.set_rng_device(rng_device)
     return eng
 
