@@ -335,3 +335,33 @@ def test_free_running_moves_leave_games_unchanged(kind, G, defer):
     assert s1['moves'] == s0['moves'] and s1['plies'] == s0['plies']
     print(f"{kind} G {G} defer {defer}: waves lockstep {s0['waves']:.0f} (extra {s0['extra_waves']:.0f}) -> "
           f"free-running {s1['waves']:.0f} (extra {s1['extra_waves']:.0f})")
+
+
+@pytest.mark.parametrize('kind,G,sched', [('seed0', 4096, 0), ('seed0', 4096 + 700, 0), ('stress5', 4096, 1)])
+def test_lag_order_leaves_games_unchanged(kind, G, sched):
+    """Round 6: which leaves a deferred-tail wave evaluates first (mtaz_set_lag_order): the least
+    advanced games first (0, the default) or round 5's lag behind the most advanced leaf (1).  Only
+    the wave each simulation runs in changes, so the records are identical bit for bit, with the same
+    evaluations + memo hits, under the default defer mode 2 (every remainder waits), in lockstep
+    (4,096 games; 4,796: the multi-chunk leaf list) and with free-running moves (chunked noise draws)."""
+    net = _net(kind)
+    out = {}
+    for order in (1, 0):
+        eng = _engine(G, 8, seed_base=500)
+        eng.set_weights(net)
+        eng.set_memo(2)
+        eng.set_defer(2)
+        eng.set_schedule(sched)
+        eng.set_lag_order(order)
+        st = eng.play()
+        assert st['schedule'] == sched
+        out[order] = (st, eng.records())
+        eng.close()
+    (s1, r1), (s0, r0) = out[1], out[0]
+    for key in ('plies', 'pos', 'action', 'k', 'codes', 'visits', 'reward', 'outcome'):
+        assert np.array_equal(r0[key], r1[key]), key
+    assert s0['nn_evals'] + s0['memo_hits'] == s1['nn_evals'] + s1['memo_hits']
+    assert s0['sims'] == s1['sims'] and s0['terminal_sims'] == s1['terminal_sims']
+    assert s0['extra_waves'] > 0
+    print(f"{kind} G {G} schedule {sched}: waves round-5 order {s1['waves']:.0f} (extra {s1['extra_waves']:.0f}) -> "
+          f"least advanced first {s0['waves']:.0f} (extra {s0['extra_waves']:.0f})")
