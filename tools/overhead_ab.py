@@ -76,7 +76,8 @@ def main():
             same = all(np.array_equal(rec[k], ref[k]) for k in ('plies', 'pos', 'action', 'visits', 'reward'))
             res[m].append({'wall_s': st['wall_ms'] / 1e3, 'trunk_ms': st['trunk_ms'], 'waves': int(st['waves']),
                            'extra_waves': int(st['extra_waves']), 'moves': int(st['moves']),
-                           'schedule': int(st['schedule']),
+                           'schedule': int(st['schedule']), 'turn_or_rng_ms': st['rng_dev_ms'],
+                           'select_ms': st['select_ms'], 'compact_ms': st['compact_ms'], 'sync_ms': st['sync_ms'],
                            'nn_evals': int(st['nn_evals']), 'memo_hits': int(st['memo_hits']),
                            'same_records': bool(same)})
             print(f'[overhead_ab] round {r} mode {m}: {res[m][-1]}', file=sys.stderr, flush=True)
