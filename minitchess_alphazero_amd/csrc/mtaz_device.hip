@@ -1273,6 +1273,10 @@ void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s) {
   hipLaunchKernelGGL(k_apply, dim3((d.pr.G + 127) / 128), dim3(128), 0, s, d, actions);
 }
 
+// Dirichlet vectors per k_turn draw in free-running play: about 40 gammas, which the wave's 64
+// attempts of one round usually cover (shape 0.6 accepts ~4 in 5)
+__device__ __forceinline__ int turn_noise_chunk(int k) { return k >= 40 ? 1 : 40 / k; }
+
 // Free-running moves (mtaz_set_schedule 1).  A game whose move is complete (all
 // `sims` simulations started, no leaf pending: its last backup ran in the previous wave) finishes
 // it here, one wavefront per game, at the start of a wave, and its next move's first simulation
@@ -1281,14 +1285,11 @@ void launch_apply(const Dev& d, const int32_t* actions, hipStream_t s) {
 //   action choice (exp/agent.py:110-119) from the root's visit counts on the game's RandomState;
 //   game step (exp/environment.py:68-82, k_apply's rules and repetition history);
 //   move start as k_move_begin (exp/agent.py:57: is the new root in the agent's table? k, new);
-//   the new move's sims - root_new Dirichlet vectors (exp/agent.py:81-82) into the game's own noise
-//   region [g * sims * KMAX, ...) with stride k.
+//   the first chunk of the new move's sims - root_new Dirichlet vectors (exp/agent.py:81-82) into the
+//   game's own noise region [g * sims * KMAX, ...) with stride k; a game in mid-move draws its next
+//   chunk here once its next simulation needs a vector not drawn yet (round 6).
 // The game's stream runs choice(move t) then noise(move t + 1), the reference's order.  `start`: the
-// play's first move of every active game (move start + noise only).
-// Dirichlet vectors per k_turn draw in free-running play: about 40 gammas, which the wave's 64
-// attempts of one round usually cover (shape 0.6 accepts ~4 in 5)
-__device__ __forceinline__ int turn_noise_chunk(int k) { return k >= 40 ? 1 : 40 / k; }
-
+// play's first move of every active game (move start + first noise chunk only).
 __global__ __launch_bounds__(64) void k_turn(Dev D, int start) {
 #pragma clang fp contract(off)
   __shared__ LegalLds s_l;
